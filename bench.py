@@ -1,0 +1,212 @@
+#!/usr/bin/env python3
+"""Benchmark: reference-equivalent env-steps/s of the fused HIP step.
+
+One "step" = one SpatialKuramoto.step() (environment/env.py:415-454) for every
+env of the batch: stim-ON + stim-OFF adaptive Dopri5 solves (~32 RHS sweeps
+of the N x N coupling), 17-19 LFP samples, the 2340-sample window update and
+the beta-band reward.  Workload: BASELINE.json configs[1] -- env0, N=1024
+oscillators x 4096 envs per GPU, synthetic (random-seeded natural
+frequencies / initial phases, reference grid coupling), actions U(-1, 1).
+
+Multi-GPU: one process per GPU (torchrun), each owning its own shard of
+4096 envs (global env id = rank*B + b seeds the env), no data-path
+collective; the only collectives are the barrier and the max-over-ranks of
+the timed region (weak scaling).
+"""
+from __future__ import annotations
+
+import argparse
+import importlib
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+PEAK_FP32_TFLOPS = 157.3   # MI355X dense FP32 (vector == matrix), MI355X_MICROARCH.md
+PEAK_HBM_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="env0", choices=["env0", "env1", "env2"])
+    ap.add_argument("--osc", type=int, default=1024)
+    ap.add_argument("--envs", type=int, default=4096, help="envs per GPU")
+    ap.add_argument("--reward", default="bbpow_action")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline sample (0 = skip)")
+    ap.add_argument("--seed", type=int, default=2024)
+    return ap.parse_args()
+
+
+def build_shard(args, rank):
+    kura = importlib.import_module("dbs-gym_amd")
+    sim_mod = importlib.import_module("dbs-gym_amd.sim")
+    base = kura.synthetic_params(args.config, args.osc) if args.osc != 512 else kura.reference_params(args.config)
+    B = args.envs
+    plist = []
+    for b in range(B):
+        gid = rank * B + b
+        p = dict(base)
+        p["rand_seed"] = args.seed + gid
+        plist.append(kura.fill_driver_arrays(p, w0_seed=10_000_000 + args.seed + gid))
+    hosts, shared = kura.build_batch(plist)
+    omega, g_stim, g_rec, theta0 = kura.reset_arrays(hosts)
+    cfg = sim_mod.make_config(base, B, reward_func=args.reward)
+    bins = kura.spectral.beta_bins(cfg.window, base["verbose_dt"])
+    ctab, stab = kura.spectral.twiddles(cfg.window, bins)
+    return cfg, shared["alpha"].astype(np.float32), omega, g_stim, g_rec, theta0, ctab, stab
+
+
+def cpu_baseline(args, cfg, alpha, omega, g_stim, g_rec, theta0, ctab, stab):
+    """The oracle (CPU restatement of step()) on this host's cores, bounded sample."""
+    from oracle import kura_oracle as ko
+    import copy
+    ncores = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    nthreads = int(os.environ.get("OMP_NUM_THREADS", ncores))
+    nb = max(1, min(nthreads, cfg.n_envs))
+    c = copy.copy(cfg)
+    c.n_envs = nb
+    o = ko.Oracle(c, alpha)
+    o.set_env_params(omega[:nb], g_stim[:nb], g_rec[:nb])
+    o.set_spectral(ctab, stab)
+    o.reset(theta0[:nb])
+    rng = np.random.default_rng(0)
+    t0 = time.perf_counter()
+    k = 0
+    while True:
+        o.step(rng.uniform(-1, 1, (nb, c.n_elec)).astype(np.float32))
+        k += 1
+        el = time.perf_counter() - t0
+        if el >= args.cpu_seconds:
+            break
+    o.close()
+    return {"value": nb * k / el, "unit": "env-steps/s", "cores": nthreads, "kind": "port",
+            "sample": f"oracle/kura_oracle.c (CPU restatement of step(), bit-exact twin of the HIP path), "
+                      f"{args.config} N={cfg.n_osc}, {nb} envs x {k} steps after reset, {el:.1f} s, "
+                      f"OpenMP {nthreads} threads (one env per thread)"}
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and rank == 0:
+        print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    sim_mod = importlib.import_module("dbs-gym_amd.sim")
+    t_setup = time.perf_counter()
+    cfg, alpha, omega, g_stim, g_rec, theta0, ctab, stab = build_shard(args, rank)
+    sim = sim_mod.KuraSim(cfg, local_rank)
+    sim.set_coupling(alpha)
+    sim.set_env_params(omega, g_stim, g_rec)
+    sim.set_spectral(ctab, stab)
+    t_setup = time.perf_counter() - t_setup
+    B, N = cfg.n_envs, cfg.n_osc
+
+    th = torch.from_numpy(theta0).to(dev)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    sim.reset(th)
+    torch.cuda.synchronize()
+    t_reset = time.perf_counter() - t0
+    reset_stats = sim.stats()
+
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(args.seed + rank)
+    acts = [torch.rand((B, cfg.n_elec), generator=gen, device=dev) * 2 - 1
+            for _ in range(args.warmup + args.steps)]
+    for k in range(args.warmup):
+        sim.step(acts[k])
+    torch.cuda.synchronize()
+
+    stream = torch.cuda.current_stream(dev)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    useful_rhs = 0
+    steps_attempted = 0
+    rejected = 0
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        ev[k][0].record(stream)
+        sim.step(acts[args.warmup + k])
+        ev[k][1].record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms = [a.elapsed_time(b) for a, b in ev]
+    st = sim.stats()  # last step's counters: [max rhs per WG, steps attempted, rejected, flags]
+    steps_attempted, rejected = int(st[1]), int(st[2])
+    # useful RHS sweeps of the last launch: 2 initial sweeps per env + 6 per attempted Dopri step
+    useful_rhs = 2 * B + 6 * steps_attempted
+    el_max = elapsed
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el_max = float(t.item())
+
+    if rank == 0:
+        value = world * B * args.steps / el_max
+        avg_kernel_s = float(np.mean(kern_ms)) / 1e3
+        flop_per_launch = useful_rhs * 4.0 * N * N   # 2 length-N dot products per oscillator per sweep
+        achieved_tf = flop_per_launch / avg_kernel_s / 1e12
+        # algorithmic HBM bytes per launch: per env theta r/w, omega, g_stim/g_rec (f64),
+        # window r/w (f64 ring + f32 obs), outputs; alpha once per launch
+        bytes_env = 8 * N + 4 * N + 8 * cfg.n_elec * N + 8 * max(cfg.n_rec, 0) * N + (8 + 8 + 4) * cfg.window + 64
+        bytes_launch = B * bytes_env + 4 * N * N
+        out = {
+            "metric": "env steps/sec (whole node), N=1024 osc x 4096 envs per GPU",
+            "value": value,
+            "unit": "env-steps/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": el_max / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (seeded reference-sampler natural frequencies, N(pi,0.6) phases, U(-1,1) actions)",
+            "config": {"workload": f"{args.config} reference step(), N={N} oscillators x {B} envs per GPU, "
+                                   f"adaptive Dopri5 rtol=atol=1e-5, W={cfg.window}, reward={args.reward}",
+                       "global_envs": world * B, "parallelism": f"env-shard x{world} (no collectives)"},
+            "roofline": {"bound": "mfma", "achieved": achieved_tf, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
+                         "frac": achieved_tf / PEAK_FP32_TFLOPS, "traffic": None,
+                         "kernel": "kura_step_kernel<4>", "avg_kernel_ms": avg_kernel_s * 1e3,
+                         "flop_per_launch": flop_per_launch, "useful_rhs_per_launch": useful_rhs,
+                         "hbm_alg_bytes_per_launch": bytes_launch,
+                         "hbm_alg_gbs": bytes_launch / avg_kernel_s / 1e9},
+            "extra": {"rhs_sweeps_per_env_step": useful_rhs / B, "dopri_steps_attempted": steps_attempted,
+                      "rejected": rejected, "phase_sweeps_per_s": world * useful_rhs / avg_kernel_s,
+                      "reset_ms": t_reset * 1e3, "reset_rhs_max": int(reset_stats[0]),
+                      "host_setup_s": t_setup},
+        }
+        if world == 1 and args.cpu_seconds > 0:
+            out["cpu_baseline"] = cpu_baseline(args, cfg, alpha, omega, g_stim, g_rec, theta0, ctab, stab)
+        else:
+            out["cpu_baseline"] = None
+        print(json.dumps(out), flush=True)
+    sim.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,23 @@
+"""dbs-gym_amd: MI355X-native batched Kuramoto environment (drop-in for
+SpatialKuramoto.step()/reset() of NevVerVer/DBS-Gym, environment/env.py).
+
+Import with ``importlib.import_module("dbs-gym_amd")`` (the directory name is
+not a Python identifier).  Numerics live in csrc/libkura.so (HIP, gfx950).
+"""
+from . import abi, configs, model_setup, spectral  # noqa: F401
+from .abi import load_library  # noqa: F401
+from .configs import reference_params, synthetic_params  # noqa: F401
+from .batch import EnvHost, build_batch, fill_driver_arrays, reset_arrays  # noqa: F401
+
+__version__ = "0.1.0"
+
+
+def __getattr__(name):
+    # torch-dependent pieces are imported lazily so host-only helpers stay cheap
+    if name in ("KuraSim", "make_config"):
+        from . import sim
+        return getattr(sim, name)
+    if name in ("KuraVectorEnv", "SpatialKuramoto"):
+        from . import vec_env
+        return getattr(vec_env, name)
+    raise AttributeError(name)

@@ -1,0 +1,145 @@
+"""ctypes mirror of include/kura.h and the loader for libkura.so.
+
+The C ABI is the drop-in boundary: Python host code
+builds a :class:`KuraConfig`, hands device pointers (``tensor.data_ptr()``) to
+``kura_step``/``kura_reset`` and never touches the numerics.  There is no CPU
+fallback: if the HIP library is missing, :func:`load_library` raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import POINTER, c_double, c_float, c_int, c_int32, c_int64, c_uint8, c_void_p
+
+KURA_ABI_VERSION = 1
+KURA_S_MAX = 32
+KURA_MAX_BINS = 32
+
+KURA_REC_NAIVE = 0
+KURA_REC_GAUSSIAN = 1
+KURA_R_BBPOW = 1
+KURA_R_TEMP_CONST = 2
+KURA_R_BBPOW_THR = 3
+
+# reward_func names of the reference (environment/env.py:323-330)
+REWARD_KINDS = {
+    "bbpow_action": KURA_R_BBPOW,
+    "temp_const_action": KURA_R_TEMP_CONST,
+    "bbpow_threth_action": KURA_R_BBPOW_THR,
+}
+# recording_kernel names (environment/env.py:333-338)
+REC_KERNELS = {"naive": KURA_REC_NAIVE, "gaussian": KURA_REC_GAUSSIAN}
+
+_ERRORS = {
+    -1: ValueError,
+    -2: RuntimeError,
+    -3: MemoryError,
+    -4: NotImplementedError,
+    -5: RuntimeError,
+}
+
+
+class KuraConfig(ctypes.Structure):
+    _fields_ = [
+        ("abi_version", c_int32),
+        ("n_osc", c_int32),
+        ("n_envs", c_int32),
+        ("window", c_int32),
+        ("n_elec", c_int32),
+        ("n_rec", c_int32),
+        ("rec_kernel", c_int32),
+        ("reward_kind", c_int32),
+        ("episode_steps", c_int32),
+        ("max_steps", c_int32),
+        ("n_bins", c_int32),
+        ("bins", c_int32 * KURA_MAX_BINS),
+        ("padlen", c_int32),
+        ("reserved_i", c_int32 * 4),
+        ("dt", c_double),
+        ("width", c_double),
+        ("pause", c_double),
+        ("transient_len", c_double),
+        ("act_lo", c_double),
+        ("act_hi", c_double),
+        ("dbs_lo", c_double),
+        ("dbs_hi", c_double),
+        ("bw_b", c_double * 5),
+        ("bw_a", c_double * 5),
+        ("bw_zi", c_double * 4),
+        ("reserved_d", c_double * 4),
+        ("rtol", c_float),
+        ("atol", c_float),
+        ("kn", c_float),
+        ("dt0", c_float),
+        ("reserved_f", c_float * 4),
+    ]
+
+
+_SYMBOLS = {
+    # name: (restype, argtypes)
+    "kura_create": (c_int, [POINTER(KuraConfig), c_int, POINTER(c_void_p)]),
+    "kura_destroy": (c_int, [c_void_p]),
+    "kura_last_error": (ctypes.c_char_p, []),
+    "kura_abi_version": (c_int, []),
+    "kura_set_coupling": (c_int, [c_void_p, c_void_p]),
+    "kura_set_env_params": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p]),
+    "kura_set_spectral": (c_int, [c_void_p, c_void_p, c_void_p]),
+    "kura_reset": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "kura_step": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                          c_void_p]),
+    "kura_reward": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p]),
+    "kura_get_state": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "kura_set_state": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "kura_get_stats": (c_int, [c_void_p, c_void_p]),
+}
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG_DIR, "csrc", "libkura.so")
+
+_lib = None
+
+
+def load_library(path: str | None = None) -> ctypes.CDLL:
+    """Load libkura.so (built by ``__graft_entry__.build()``).  Raises if absent."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise RuntimeError(
+            f"libkura.so not found at {p}: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+            "(the HIP library is the only implementation of the step path; there is no CPU fallback)")
+    lib = ctypes.CDLL(p)
+    for name, (res, args) in _SYMBOLS.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.kura_abi_version() != KURA_ABI_VERSION:
+        raise RuntimeError("libkura ABI version mismatch")
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def check(lib: ctypes.CDLL, rc: int, what: str) -> None:
+    if rc != 0:
+        msg = lib.kura_last_error()
+        msg = msg.decode() if msg else ""
+        raise _ERRORS.get(rc, RuntimeError)(f"{what} failed ({rc}): {msg}")
+
+
+def ptr(a) -> int | None:
+    """Raw address of a numpy array or torch tensor (None passes NULL)."""
+    if a is None:
+        return None
+    if hasattr(a, "data_ptr"):
+        return a.data_ptr()
+    return a.ctypes.data
+
+
+__all__ = [
+    "KuraConfig", "load_library", "check", "ptr", "LIB_PATH",
+    "KURA_ABI_VERSION", "KURA_S_MAX", "KURA_MAX_BINS", "REWARD_KINDS", "REC_KERNELS",
+    "KURA_REC_NAIVE", "KURA_REC_GAUSSIAN", "KURA_R_BBPOW", "KURA_R_TEMP_CONST", "KURA_R_BBPOW_THR",
+    "c_int64", "c_uint8",
+]

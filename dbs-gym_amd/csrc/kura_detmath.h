@@ -1,0 +1,160 @@
+// kura_detmath.h -- deterministic IEEE-754 primitives for the Kuramoto step.
+//
+// Why this file exists: the reference RHS (environment/env.py:252-256) is
+// integrated by an adaptive Dopri5 whose dense-output polynomial cancels
+// catastrophically in fp32 (diffrax FourthOrderPolynomialInterpolation, see
+// DESIGN.md "Numerics"). A 1-ulp difference anywhere in the pipeline grows
+// to ~1 rad after 1000 env-steps, so the 1e-5-relative phase gate of
+// BASELINE.json can only be met by a GPU path that is a *bit-exact twin* of
+// the CPU oracle. Every transcendental used on the path is therefore defined
+// here from +,-,*,fma,rint,trunc only (all exactly specified by IEEE-754 on
+// both gfx950 and x86-64), and the same header is compiled by hipcc (device)
+// and gcc (oracle/). Both sides must be built with -ffp-contract=off.
+//
+// Accuracy (checked by tests/test_detmath.py against libm in double):
+//   kdm_sincosf  <= 2 ulp on |x| < 1e4 (Cody-Waite 3-part pi/2, Cephes polys)
+//   kdm_fmod2pi  exact (== fmodf(y, (float)(2*pi)), as jnp.fmod in env.py:253)
+//   kdm_inv_fifth_root  ~0.5 ulp after rounding to float
+#pragma once
+
+#if defined(__HIPCC__) || defined(__HIP__)
+#include <hip/hip_runtime.h>
+#define KDM_FN __host__ __device__ static inline
+#define KDM_FMAF(a, b, c) __builtin_fmaf((a), (b), (c))
+#define KDM_FMA(a, b, c) __builtin_fma((a), (b), (c))
+#else
+#include <math.h>
+#include <stdint.h>
+#define KDM_FN static inline
+#define KDM_FMAF(a, b, c) fmaf((a), (b), (c))
+#define KDM_FMA(a, b, c) fma((a), (b), (c))
+#endif
+
+#if defined(__clang__)
+#pragma clang fp contract(off)
+#endif
+
+// (float)(2*pi): jnp.fmod(y, 2*jnp.pi) with x64 disabled divides by this.
+#define KDM_TWO_PI_F 6.28318548202514648438f      /* 0x1.921fb6p+2 */
+#define KDM_INV_TWO_PI_F 0.15915493667125701904f  /* 0x1.45f306p-3 */
+#define KDM_TWO_OVER_PI_F 0.63661974668502807617f /* 0x1.45f306p-1 */
+// pi/2 = C1 + C2 + C3 (+1e-23), each a float; products with an integer
+// quadrant count are exact inside fmaf.
+#define KDM_PIO2_C1 1.57079637050628662109f       /* 0x1.921fb6p+0 */
+#define KDM_PIO2_C2 (-4.37113882867379290890e-08f) /* -0x1.777a5cp-25 */
+#define KDM_PIO2_C3 (-1.71512451884415714046e-15f) /* -0x1.ee59dap-50 */
+
+// Exact fmodf(y, KDM_TWO_PI_F).  Result has the sign of y (C / jnp.fmod).
+// For |y| < 2^22 the quotient estimate is off by at most one and the
+// remainder computed by fmaf is exact; larger |y| takes the
+// classic shift-subtract path, which is exact by Sterbenz's lemma.
+KDM_FN float kdm_fmod2pi(float y) {
+    const float d = KDM_TWO_PI_F;
+    float ay = y < 0.0f ? -y : y;
+    float r;
+    if (ay < 4194304.0f) {
+        float q = truncf(ay * KDM_INV_TWO_PI_F);
+        r = KDM_FMAF(-q, d, ay);
+        if (r < 0.0f) r += d;
+        else if (r >= d) r -= d;
+    } else {
+        r = ay;
+        if (!(r < 3.0e38f)) return (y - y) / (y - y);  // inf/nan -> nan
+        // scale d up by powers of two until just below r, then subtract down
+        float dd = d;
+        int e = 0;
+        while (dd * 2.0f <= r) { dd *= 2.0f; ++e; }
+        for (; e >= 0; --e) {
+            if (r >= dd) r -= dd;
+            dd *= 0.5f;
+        }
+    }
+    return y < 0.0f ? -r : r;
+}
+
+// sin and cos of x (any float with |x| < ~1e5 for full accuracy).
+KDM_FN void kdm_sincosf(float x, float* s_out, float* c_out) {
+    float j = rintf(x * KDM_TWO_OVER_PI_F);
+    float r = KDM_FMAF(-j, KDM_PIO2_C1, x);
+    r = KDM_FMAF(-j, KDM_PIO2_C2, r);
+    r = KDM_FMAF(-j, KDM_PIO2_C3, r);
+    int q = ((int)j) & 3;
+    float z = r * r;
+    // Cephes sinf/cosf minimax polynomials on [-pi/4, pi/4]
+    float ps = KDM_FMAF(z, -1.9515295891e-4f, 8.3321608736e-3f);
+    ps = KDM_FMAF(z, ps, -1.6666654611e-1f);
+    float sr = KDM_FMAF(r * z, ps, r);
+    float pc = KDM_FMAF(z, 2.443315711809948e-5f, -1.388731625493765e-3f);
+    pc = KDM_FMAF(z, pc, 4.166664568298827e-2f);
+    float cr = KDM_FMAF(z * z, pc, KDM_FMAF(-0.5f, z, 1.0f));
+    float s, c;
+    switch (q) {
+        case 0: s = sr; c = cr; break;
+        case 1: s = cr; c = -sr; break;
+        case 2: s = -sr; c = -cr; break;
+        default: s = -cr; c = sr; break;
+    }
+    *s_out = s;
+    *c_out = c;
+}
+
+KDM_FN float kdm_cosf(float x) {
+    float s, c;
+    kdm_sincosf(x, &s, &c);
+    return c;
+}
+
+// x^(-1/5) for finite x > 0, rounded to float.  Only +,*,fma and exact
+// power-of-two scaling are used, so host and device agree bit for bit.
+// Special values follow pow(): x == 0 -> +inf, x == +inf -> 0, nan -> nan.
+KDM_FN float kdm_inv_fifth_root(float xf) {
+    if (xf != xf) return xf;
+    if (xf <= 0.0f) return (xf == 0.0f) ? __builtin_inff() : (xf - xf) / (xf - xf);
+    if (xf > 3.40282346638528859812e+38f) return 0.0f;
+    // decompose x = m * 2^e with m in [1, 2) using the float bit pattern
+    union { float f; uint32_t u; } cv;
+    cv.f = xf;
+    int e;
+    double m;
+    uint32_t bexp = (cv.u >> 23) & 0xffu;
+    if (bexp == 0) {  // subnormal float: normalise in double
+        double xd = (double)xf * 18014398509481984.0;  // 2^54
+        union { double d; uint64_t u; } dv;
+        dv.d = xd;
+        e = (int)((dv.u >> 52) & 0x7ffu) - 1023 - 54;
+        dv.u = (dv.u & 0x000fffffffffffffULL) | 0x3ff0000000000000ULL;
+        m = dv.d;
+    } else {
+        e = (int)bexp - 127;
+        union { float f; uint32_t u; } mv;
+        mv.u = (cv.u & 0x007fffffu) | 0x3f800000u;
+        m = (double)mv.f;
+    }
+    // e = 5*q + r with r in [0, 5)
+    int qd = (e >= 0) ? e / 5 : -((-e + 4) / 5);
+    int r = e - 5 * qd;
+    // w ~ m^(-1/5) on [1, 2): linear start (rel err < 1.2%) + Newton
+    //   w <- w * (1 + (1 - m w^5) / 5)
+    double w = KDM_FMA(-0.1236, m, 1.1195);
+    for (int it = 0; it < 6; ++it) {
+        double w2 = w * w;
+        double w5 = w2 * w2 * w;
+        double t = KDM_FMA(-m, w5, 1.0);
+        w = KDM_FMA(w * 0.2, t, w);
+    }
+    // 2^(-r/5) for r = 0..4
+    const double inv_tab[5] = {1.0, 0x1.bdb8cdadbe120p-1, 0x1.8406003b2ae5cp-1,
+                               0x1.51cb453b9536cp-1, 0x1.2611186bae675p-1};
+    double y = w * inv_tab[r];
+    // multiply by 2^(-qd) exactly (|qd| <= 30 for float inputs)
+    union { double d; uint64_t u; } sc;
+    sc.u = (uint64_t)(1023 - qd) << 52;
+    return (float)(y * sc.d);
+}
+
+// ---- canonical reductions ---------------------------------------------
+// R64: the order in which every per-env sum over oscillators is taken.
+// lane l (0..63) accumulates x[l], x[l+64], x[l+128], ... in ascending order
+// (starting from +0), then lanes combine by an xor butterfly with offsets
+// 32,16,8,4,2,1 (p[l] = p[l] + p[l^o]).  This is exactly what one wavefront
+// does with a strided loop + __shfl_xor; the oracle replays it sequentially.

@@ -1,0 +1,185 @@
+"""KuraSim: thin owner of one libkura handle (one GPU, B environments).
+
+This is the seam the reference's ``KuramotoJAX.forward`` + ``SpatialKuramoto``
+step/reset occupy (env.py:260-271, :415-454, :467-614).  All numerics run in
+the HIP library; this class only allocates PyTorch-ROCm tensors (storage),
+passes raw device pointers through the C ABI and maps error codes to the
+reference's exception types.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import torch
+
+from . import abi
+from . import spectral
+from .abi import KURA_S_MAX, KuraConfig, check, ptr
+
+
+def make_config(params: dict, n_envs: int, reward_func: str | None = None, max_steps: int = 4096) -> KuraConfig:
+    """Build the C config from a reference params dict (env.py:277-338)."""
+    p = params
+    step_len = p["electrode_width"] + p["electrode_pause"]                      # env.py:294
+    wind_len = step_len * p["observe_wind_counts"]                               # env.py:296
+    W = int(wind_len / p["verbose_dt"])                                          # env.py:297
+    if p["transient_state_len"] < wind_len:                                      # env.py:303-304
+        raise ValueError("Transient state should be longer than RL agent observation window!")
+    rf = reward_func if reward_func is not None else p.get("reward_func")
+    if rf not in abi.REWARD_KINDS:                                               # env.py:323-330
+        raise ValueError("Wrong reward function!")
+    if p["recording_kernel"] not in abi.REC_KERNELS:                            # env.py:333-338
+        raise ValueError("Wrong recording kernel function!")
+    if len(p["electrode_amps"]) != len(p["elec_coords"]):                        # env.py:91
+        raise AssertionError("Number of amplitudes is not equal to number of electrode coordinates!")
+    c = KuraConfig()
+    c.abi_version = abi.KURA_ABI_VERSION
+    c.n_osc = int(p["num_oscillators"])
+    c.n_envs = int(n_envs)
+    c.window = W
+    c.n_elec = len(p["elec_coords"])
+    c.n_rec = len(p["rec_coords"])
+    c.rec_kernel = abi.REC_KERNELS[p["recording_kernel"]]
+    c.reward_kind = abi.REWARD_KINDS[rf]
+    c.episode_steps = int(p["total_episode_len"] / step_len)                     # env.py:300
+    c.max_steps = int(max_steps)
+    bins = spectral.beta_bins(W, p["verbose_dt"])
+    if len(bins) > abi.KURA_MAX_BINS:
+        raise ValueError("too many beta-band bins")
+    c.n_bins = len(bins)
+    for i, b in enumerate(bins):
+        c.bins[i] = int(b)
+    b, a, zi = spectral.butter_bandpass(p["verbose_dt"])
+    c.padlen = 3 * max(len(a), len(b))                                           # scipy filtfilt default
+    for i in range(5):
+        c.bw_b[i] = float(b[i])
+        c.bw_a[i] = float(a[i])
+    for i in range(4):
+        c.bw_zi[i] = float(zi[i])
+    c.dt = float(p["verbose_dt"])
+    c.width = float(p["electrode_width"])
+    c.pause = float(p["electrode_pause"])
+    c.transient_len = float(p["transient_state_len"])
+    c.act_lo, c.act_hi = -1.0, 1.0                                               # env.py:309
+    c.dbs_lo, c.dbs_hi = float(p["dbs_action_bounds"][0]), float(p["dbs_action_bounds"][1])
+    c.rtol = c.atol = np.float32(1e-5)                                           # env.py:249
+    c.kn = np.float32(p["K"] / p["num_oscillators"])                            # env.py:264
+    c.dt0 = np.float32(0.05)                                                     # env.py:267
+    return c
+
+
+class KuraSim:
+    """B environments on one GPU behind libkura."""
+
+    def __init__(self, cfg: KuraConfig, device: torch.device | str | int = 0):
+        if not torch.cuda.is_available():
+            raise RuntimeError("KuraSim needs a ROCm GPU (torch.cuda.is_available() is False); "
+                               "there is no CPU implementation of the step path")
+        self.lib = abi.load_library()
+        self.cfg = cfg
+        self.device = torch.device("cuda", torch.device(device).index if not isinstance(device, int) else device)
+        if self.device.index is None:
+            self.device = torch.device("cuda", 0)
+        self.B, self.N, self.W = cfg.n_envs, cfg.n_osc, cfg.window
+        h = ctypes.c_void_p()
+        with torch.cuda.device(self.device):
+            check(self.lib, self.lib.kura_create(ctypes.byref(cfg), self.device.index, ctypes.byref(h)), "kura_create")
+        self._h = h
+        dev = self.device
+        B = self.B
+        self.obs = torch.zeros((B, self.W), dtype=torch.float32, device=dev)
+        self.reward = torch.zeros(B, dtype=torch.float64, device=dev)
+        self.done = torch.zeros(B, dtype=torch.uint8, device=dev)
+        self.lfp_true = torch.zeros((B, KURA_S_MAX), dtype=torch.float32, device=dev)
+        self.lfp_rec = torch.zeros((B, KURA_S_MAX), dtype=torch.float64, device=dev)
+        self.nsamp = torch.zeros(B, dtype=torch.int32, device=dev)
+
+    # ---- setup --------------------------------------------------------------
+    def set_coupling(self, alpha: np.ndarray) -> None:
+        a = np.ascontiguousarray(alpha, dtype=np.float32)
+        if a.shape != (self.N, self.N):
+            raise ValueError(f"alpha shape {a.shape} != ({self.N}, {self.N})")
+        check(self.lib, self.lib.kura_set_coupling(self._h, a.ctypes.data), "kura_set_coupling")
+
+    def set_env_params(self, omega, g_stim, g_rec=None, env0: int = 0) -> None:
+        w = np.ascontiguousarray(omega, dtype=np.float32)
+        n = w.shape[0]
+        gs = np.ascontiguousarray(g_stim, dtype=np.float64)
+        gr = None if g_rec is None else np.ascontiguousarray(g_rec, dtype=np.float64)
+        check(self.lib, self.lib.kura_set_env_params(self._h, env0, n, w.ctypes.data, gs.ctypes.data,
+                                                     None if gr is None else gr.ctypes.data),
+              "kura_set_env_params")
+
+    def set_spectral(self, cos_tab, sin_tab) -> None:
+        c = np.ascontiguousarray(cos_tab, dtype=np.float64)
+        s = np.ascontiguousarray(sin_tab, dtype=np.float64)
+        check(self.lib, self.lib.kura_set_spectral(self._h, c.ctypes.data, s.ctypes.data), "kura_set_spectral")
+
+    # ---- hot path -------------------------------------------------------------
+    def _stream(self):
+        return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    def reset(self, theta0: torch.Tensor, mask: torch.Tensor | None = None) -> torch.Tensor:
+        th = theta0.to(self.device, torch.float32).contiguous()
+        if th.shape != (self.B, self.N):
+            raise ValueError("theta0 must be (B, N)")
+        m = None if mask is None else mask.to(self.device, torch.uint8).contiguous()
+        with torch.cuda.device(self.device):
+            check(self.lib, self.lib.kura_reset(self._h, ptr(m), ptr(th), ptr(self.obs), self._stream()),
+                  "kura_reset")
+        self._keep = (th, m)  # keep inputs alive until the stream consumes them
+        return self.obs
+
+    def step(self, action: torch.Tensor):
+        a = action.to(self.device, torch.float32).contiguous()
+        if a.numel() != self.B * self.cfg.n_elec:
+            raise ValueError("action must have B * n_elec elements")
+        with torch.cuda.device(self.device):
+            check(self.lib, self.lib.kura_step(self._h, ptr(a), ptr(self.obs), ptr(self.reward), ptr(self.done),
+                                               ptr(self.lfp_true), ptr(self.lfp_rec), ptr(self.nsamp),
+                                               self._stream()), "kura_step")
+        self._keep = (a,)
+        return self.obs, self.reward, self.done
+
+    def reward_of(self, window: torch.Tensor, u0: torch.Tensor) -> torch.Tensor:
+        w = window.to(self.device, torch.float64).contiguous()
+        u = u0.to(self.device, torch.float32).contiguous()
+        n = w.shape[0]
+        out = torch.empty(n, dtype=torch.float64, device=self.device)
+        with torch.cuda.device(self.device):
+            check(self.lib, self.lib.kura_reward(self._h, ptr(w), ptr(u), ptr(out), n, self._stream()),
+                  "kura_reward")
+        return out
+
+    # ---- state ------------------------------------------------------------------
+    def get_state(self) -> dict:
+        B, N, W = self.B, self.N, self.W
+        st = dict(y=np.empty((B, N), np.float32), t=np.empty(B, np.float64), step=np.empty(B, np.int32),
+                  ring=np.empty((B, W), np.float64), wpos=np.empty(B, np.int32))
+        check(self.lib, self.lib.kura_get_state(self._h, st["y"].ctypes.data, st["t"].ctypes.data,
+                                                st["step"].ctypes.data, st["ring"].ctypes.data,
+                                                st["wpos"].ctypes.data), "kura_get_state")
+        return st
+
+    def set_state(self, st: dict) -> None:
+        arrs = [np.ascontiguousarray(st["y"], np.float32), np.ascontiguousarray(st["t"], np.float64),
+                np.ascontiguousarray(st["step"], np.int32), np.ascontiguousarray(st["ring"], np.float64),
+                np.ascontiguousarray(st["wpos"], np.int32)]
+        check(self.lib, self.lib.kura_set_state(self._h, *[a.ctypes.data for a in arrs]), "kura_set_state")
+
+    def stats(self) -> np.ndarray:
+        out = np.zeros(4, np.int64)
+        check(self.lib, self.lib.kura_get_stats(self._h, out.ctypes.data), "kura_get_stats")
+        return out
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            self.lib.kura_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

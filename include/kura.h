@@ -1,0 +1,134 @@
+/*
+ * kura.h -- C ABI of libkura, the MI355X-native batched Kuramoto simulator
+ * that replaces SpatialKuramoto.step()/reset() of the reference
+ * (environment/env.py:415-454 and :467-614).
+ *
+ * One handle owns B independent environments on one GPU.  All per-step I/O
+ * pointers are DEVICE pointers allocated by the caller (PyTorch-ROCm tensors
+ * via tensor.data_ptr()); they are borrowed for the duration of the call and
+ * the work is enqueued on the given hipStream_t (NULL = default stream).
+ * Setup calls take HOST pointers and are synchronous.  No call allocates
+ * device memory except kura_create.  Errors never throw across the ABI: every
+ * call returns 0 on success or a negative KURA_E* code, and
+ * kura_last_error() returns a thread-local message.
+ *
+ * Reference interfaces each entry point replaces (file:line under the
+ * reference tree):
+ *   kura_create          SpatialKuramoto.__init__        env.py:277-386
+ *   kura_set_coupling    KuramotoJAX.__init__ alpha     env.py:219-229
+ *   kura_set_env_params  apply_locus_mask + SimpleDBS    env.py:566-593, :61-156
+ *   kura_set_spectral    calc_beta_band_power bins       utils.py:21-27
+ *   kura_reset           SpatialKuramoto.reset transient env.py:594-614
+ *   kura_step            SpatialKuramoto.step            env.py:415-454
+ *   kura_reward          reward_* on a given window      env.py:638-688
+ *   kura_get/set_state   (no reference equivalent; env state was not
+ *                        checkpointable)
+ */
+#ifndef KURA_H
+#define KURA_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KURA_ABI_VERSION 1
+#define KURA_S_MAX 32   /* max LFP samples emitted by one step (ref: 17-19) */
+#define KURA_MAX_BINS 32
+
+enum {
+    KURA_OK = 0,
+    KURA_E_INVALID = -1,   /* bad argument (ref: ValueError/AssertionError) */
+    KURA_E_HIP = -2,       /* HIP runtime error */
+    KURA_E_NOMEM = -3,
+    KURA_E_UNSUPPORTED = -4,
+    KURA_E_STATE = -5      /* call order violated (e.g. step before reset) */
+};
+
+enum { KURA_REC_NAIVE = 0, KURA_REC_GAUSSIAN = 1 };             /* env.py:333-338 */
+enum { KURA_R_BBPOW = 1, KURA_R_TEMP_CONST = 2, KURA_R_BBPOW_THR = 3 }; /* env.py:323-330 */
+
+typedef struct KuraConfig {
+    int32_t abi_version;   /* must be KURA_ABI_VERSION */
+    int32_t n_osc;         /* N, params_dict['num_oscillators'] */
+    int32_t n_envs;        /* B, environments in this handle */
+    int32_t window;        /* W = int(step_len*observe_wind_counts/verbose_dt), env.py:294-297 */
+    int32_t n_elec;        /* stimulating contacts = len(elec_coords), env.py:93-95 */
+    int32_t n_rec;         /* recording contacts = len(rec_coords), env.py:96-98 */
+    int32_t rec_kernel;    /* KURA_REC_* */
+    int32_t reward_kind;   /* KURA_R_* */
+    int32_t episode_steps; /* total_episode_counts, env.py:300 */
+    int32_t max_steps;     /* diffrax diffeqsolve max_steps default (4096) */
+    int32_t n_bins;        /* rfft bins with beta_a < f < beta_b (utils.py:24-26) */
+    int32_t bins[KURA_MAX_BINS];
+    int32_t padlen;        /* filtfilt padlen for R2 (3*max(len(a),len(b)) = 15) */
+    int32_t reserved_i[4];
+    double dt;             /* verbose_dt: save-grid spacing (units) */
+    double width;          /* electrode_width: stimulation ON interval */
+    double pause;          /* electrode_pause: OFF interval */
+    double transient_len;  /* transient_state_len */
+    double act_lo, act_hi; /* ppo_action_bounds  [-1, 1]  env.py:309 */
+    double dbs_lo, dbs_hi; /* dbs_action_bounds  [-5, 5]  env.py:308 */
+    double bw_b[5];        /* butter(2, [12, 30]/(fs/2), 'band') numerator  (utils.py:812) */
+    double bw_a[5];        /* ... denominator */
+    double bw_zi[4];       /* scipy.signal.lfilter_zi(b, a) */
+    double reserved_d[4];
+    float rtol, atol;      /* PIDController(rtol=1e-5, atol=1e-5), env.py:249 */
+    float kn;              /* float32(K / N), env.py:264 */
+    float dt0;             /* diffeqsolve dt0 = 0.05, env.py:267 */
+    float reserved_f[4];
+} KuraConfig;
+
+typedef struct KuraHandle KuraHandle;
+
+/* create / destroy */
+int kura_create(const KuraConfig* cfg, int device, KuraHandle** out);
+int kura_destroy(KuraHandle* h);
+const char* kura_last_error(void);
+int kura_abi_version(void);
+
+/* setup (host pointers, synchronous) */
+int kura_set_coupling(KuraHandle* h, const float* alpha /* N*N row-major, alpha[i][j] */);
+int kura_set_env_params(KuraHandle* h, int env0, int n,
+                        const float* omega,   /* n*N  (float32 cast of w0, env.py:264) */
+                        const double* g_stim, /* n*n_elec*N conductances, env.py:106-120 */
+                        const double* g_rec); /* n*n_rec*N  recorder conductances, :142-156 */
+int kura_set_spectral(KuraHandle* h, const double* cos_tab, const double* sin_tab /* n_bins*W */);
+
+/* hot path (device pointers, asynchronous on stream) */
+int kura_reset(KuraHandle* h, const uint8_t* mask /* B or NULL = all */,
+               const float* theta0 /* B*N float32 initial phases */,
+               float* obs /* B*W or NULL */, void* stream);
+int kura_step(KuraHandle* h, const float* action /* B*n_elec in [-1,1] */,
+              float* obs,       /* B*W   float32 window, oldest first */
+              double* reward,   /* B     */
+              uint8_t* done,    /* B     */
+              float* lfp_true,  /* B*KURA_S_MAX  theta_mean (naive LFP), env.py:444 */
+              double* lfp_rec,  /* B*KURA_S_MAX  theta_records, env.py:445 (may be NULL) */
+              int32_t* nsamp,   /* B     samples emitted this step (17..19) */
+              void* stream);
+int kura_reward(KuraHandle* h, const double* window /* n*W device */, const float* u0 /* n device */,
+                double* reward /* n device */, int n, void* stream);
+
+/* state snapshot for checkpoint/resume and parity tests (host pointers; syncs) */
+int kura_get_state(KuraHandle* h, float* y /* B*N */, double* t /* B */, int32_t* step /* B */,
+                   double* ring /* B*W */, int32_t* wpos /* B */);
+int kura_set_state(KuraHandle* h, const float* y, const double* t, const int32_t* step,
+                   const double* ring, const int32_t* wpos);
+/* counters: [0] RHS sweeps issued per env (max over envs) in the last call,
+ * [1] Dopri5 steps attempted, [2] rejected, [3] error flags (bit0 max_steps, bit1 nan) */
+int kura_get_stats(KuraHandle* h, int64_t* out4);
+
+/* diagnostics for the GPU parity tests (host pointers; synchronous; not on
+ * the step path).  selftest_math writes 8 floats per element: sin, cos,
+ * fmod2pi, inv_fifth_root(|y|), sqrt(|x|), x/y, f32(f64 x / f64 y),
+ * ceil(x/0.05).  selftest_gemm runs the production MFMA coupling GEMM on one
+ * 32 x N operand: Y[r][i] = sum_k X[r][k] * alpha[i][k]. */
+int kura_selftest_math(const float* x, const float* y, float* out, int n);
+int kura_selftest_gemm(const float* X, const float* alpha, float* Y, int N);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* KURA_H */

@@ -1,0 +1,673 @@
+/*
+ * kura_oracle.c -- CPU restatement of SpatialKuramoto.step()/reset()
+ * (reference: environment/env.py) used ONLY as the parity checker and as
+ * bench.py's cpu_baseline.  TEST INFRASTRUCTURE: nothing on the product path
+ * (dbs-gym_amd/) may link or call this file.
+ *
+ * What it restates, with the reference line each piece follows:
+ *   rhs()          KuramotoJAX.dynamics                 env.py:252-256
+ *   solve()        KuramotoJAX.forward -> diffrax.diffeqsolve(Dopri5,
+ *                  PIDController(1e-5,1e-5), dt0=0.05, SaveAt(ts))
+ *                                                       env.py:247-249,260-271
+ *                  diffrax 0.7.0 semantics (third-party, absent here; pinned
+ *                  version requirements_pip.txt:12): Dormand-Prince 5(4)
+ *                  tableau with the Shampine error weights, FSAL, increments
+ *                  k = h*f, I-controller (icoeff=1, exponent 1/5, safety 0.9,
+ *                  factormin 0.2, factormax 10, accepted steps never shrink),
+ *                  RMS error norm of err/(atol + rtol*max|y0|,|y1|),
+ *                  _clip_to_end(1e-6), saves by the 4th-order dense
+ *                  interpolant (_Dopri5Interpolation.c_mid).  Time is fp32
+ *                  because jax x64 is disabled in the reference.
+ *   arange()       np.arange in step()/reset()          env.py:426-441,606-609
+ *   pulse          rescale_action + sum g_e*u_e         env.py:389-393,419-424
+ *   lfp            calc_naive_lfp / calc_distance_lfp   env.py:396-412
+ *   window         np.append + [-W:]                    env.py:447-448
+ *   rewards R1/R2/R3                                    env.py:638-688,
+ *                  calc_beta_band_power utils.py:21-27, band_pass_envelope
+ *                  utils.py:794-816 (filtfilt 'odd' pad, lfilter DF2T)
+ *
+ * Arithmetic contract shared with the HIP kernels (DESIGN.md "Numerics"):
+ * every fp32/fp64 operation below is performed in the same order, with the
+ * same fused multiply-adds, as dbs-gym_amd/csrc/kura_kernels.hip, and the
+ * transcendentals come from kura_detmath.h.  Build with -ffp-contract=off.
+ * Parity with the *reference* solver is statistical only (diffrax absent);
+ * plumbing around the solver is pinned by tests/golden (stub-imported
+ * reference with this solver plugged in).
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../include/kura.h"
+#include "../dbs-gym_amd/csrc/kura_detmath.h"
+
+#define ORACLE_VERSION 1
+
+/* ---- Dopri5 tableau (diffrax _dopri5_tableau), cast to fp32 as jnp does --- */
+#define F(x) ((float)(x))
+static const float A21 = F(1.0 / 5.0);
+static const float A31 = F(3.0 / 40.0), A32 = F(9.0 / 40.0);
+static const float A41 = F(44.0 / 45.0), A42 = F(-56.0 / 15.0), A43 = F(32.0 / 9.0);
+static const float A51 = F(19372.0 / 6561.0), A52 = F(-25360.0 / 2187.0),
+                   A53 = F(64448.0 / 6561.0), A54 = F(-212.0 / 729.0);
+static const float A61 = F(9017.0 / 3168.0), A62 = F(-355.0 / 33.0), A63 = F(46732.0 / 5247.0),
+                   A64 = F(49.0 / 176.0), A65 = F(-5103.0 / 18656.0);
+static const float A71 = F(35.0 / 384.0), A73 = F(500.0 / 1113.0), A74 = F(125.0 / 192.0),
+                   A75 = F(-2187.0 / 6784.0), A76 = F(11.0 / 84.0);
+static const float E1 = F(35.0 / 384.0 - 1951.0 / 21600.0), E3 = F(500.0 / 1113.0 - 22642.0 / 50085.0),
+                   E4 = F(125.0 / 192.0 - 451.0 / 720.0), E5 = F(-2187.0 / 6784.0 + 12231.0 / 42400.0),
+                   E6 = F(11.0 / 84.0 - 649.0 / 6300.0), E7 = F(-1.0 / 60.0);
+static const float M1 = F(6025192743.0 / 30085553152.0 / 2.0), M3 = F(51252292925.0 / 65400821598.0 / 2.0),
+                   M4 = F(-2691868925.0 / 45128329728.0 / 2.0),
+                   M5 = F(187940372067.0 / 1594534317056.0 / 2.0),
+                   M6 = F(-1776094331.0 / 19743644256.0 / 2.0), M7 = F(11237099.0 / 235043384.0 / 2.0);
+#undef F
+
+/* ---------------------------------------------------------------- helpers */
+int oracle_version(void) { return ORACLE_VERSION; }
+
+/* R64 canonical reductions (kura_detmath.h) */
+float oracle_r64_f32(const float* x, int n) {
+    float p[64];
+    for (int l = 0; l < 64; ++l) {
+        float a = 0.0f;
+        for (int i = l; i < n; i += 64) a = a + x[i];
+        p[l] = a;
+    }
+    for (int o = 32; o >= 1; o >>= 1) {
+        float q[64];
+        for (int l = 0; l < 64; ++l) q[l] = p[l] + p[l ^ o];
+        memcpy(p, q, sizeof(p));
+    }
+    return p[0];
+}
+
+double oracle_r64_f64(const double* x, int n) {
+    double p[64];
+    for (int l = 0; l < 64; ++l) {
+        double a = 0.0;
+        for (int i = l; i < n; i += 64) a = a + x[i];
+        p[l] = a;
+    }
+    for (int o = 32; o >= 1; o >>= 1) {
+        double q[64];
+        for (int l = 0; l < 64; ++l) q[l] = p[l] + p[l ^ o];
+        memcpy(p, q, sizeof(p));
+    }
+    return p[0];
+}
+
+static double r64_dot_f64(const double* x, const double* w, int n) {
+    double p[64];
+    for (int l = 0; l < 64; ++l) {
+        double a = 0.0;
+        for (int i = l; i < n; i += 64) a = fma(x[i], w[i], a);
+        p[l] = a;
+    }
+    for (int o = 32; o >= 1; o >>= 1) {
+        double q[64];
+        for (int l = 0; l < 64; ++l) q[l] = p[l] + p[l ^ o];
+        memcpy(p, q, sizeof(p));
+    }
+    return p[0];
+}
+
+/* np.arange(start, stop, step) in float64 (numpy PyArray_Arange + DOUBLE_fill):
+ * n = ceil((stop-start)/step); x[0] = start; x[i] = start + i*((start+step)-start). */
+typedef struct { double start, delta; int n; const double* vals; } Grid;
+
+static Grid arange(double start, double stop, double step) {
+    Grid g;
+    double len = ceil((stop - start) / step);
+    g.n = len > 0.0 ? (int)len : 0;
+    g.start = start;
+    g.delta = (start + step) - start;
+    g.vals = NULL;
+    return g;
+}
+static double grid_at(const Grid* g, int i) {
+    if (g->vals) return g->vals[i];
+    return i == 0 ? g->start : g->start + (double)i * g->delta;
+}
+
+/* exported for golden tests */
+int oracle_arange(double start, double stop, double step, double* out, int cap) {
+    Grid g = arange(start, stop, step);
+    for (int i = 0; i < g.n && i < cap; ++i) out[i] = grid_at(&g, i);
+    return g.n;
+}
+
+/* --------------------------------------------------------------- context */
+typedef struct {
+    KuraConfig cfg;
+    int N;
+    float* alphaT; /* alphaT[j*N + i] = alpha[i][j] */
+} OCtx;
+
+void* oracle_create(const KuraConfig* cfg, const float* alpha) {
+    OCtx* o = (OCtx*)calloc(1, sizeof(OCtx));
+    if (!o) return NULL;
+    o->cfg = *cfg;
+    o->N = cfg->n_osc;
+    int N = o->N;
+    o->alphaT = (float*)malloc(sizeof(float) * (size_t)N * N);
+    if (!o->alphaT) { free(o); return NULL; }
+    for (int i = 0; i < N; ++i)
+        for (int j = 0; j < N; ++j) o->alphaT[(size_t)j * N + i] = alpha[(size_t)i * N + j];
+    return o;
+}
+
+void oracle_destroy(void* p) {
+    OCtx* o = (OCtx*)p;
+    if (!o) return;
+    free(o->alphaT);
+    free(o);
+}
+
+/* Work buffers for one env (one OpenMP thread). */
+typedef struct {
+    float *s, *c, *P, *Q;
+    float *F[7];          /* f at each stage; F[0] = FSAL f(y0) */
+    float *y0, *ys, *y1;  /* step start, stage input, 7th stage input */
+    float *ca, *cb, *cc;  /* dense-output coefficients */
+    float *row;           /* a saved row */
+    float *cosrow;
+    float *zero;          /* pulse = 0 (stim OFF), env.py:434 */
+    double *prod;
+} Work;
+
+static int work_alloc(Work* w, int N) {
+    size_t nf = (size_t)N;
+    float** fl[] = {&w->s, &w->c, &w->P, &w->Q, &w->y0, &w->ys, &w->y1, &w->ca, &w->cb, &w->cc, &w->row, &w->cosrow, &w->zero};
+    for (size_t i = 0; i < sizeof(fl) / sizeof(fl[0]); ++i) {
+        *fl[i] = (float*)malloc(sizeof(float) * nf);
+        if (!*fl[i]) return -1;
+    }
+    for (size_t i = 0; i < nf; ++i) w->zero[i] = 0.0f;
+    for (int k = 0; k < 7; ++k) {
+        w->F[k] = (float*)malloc(sizeof(float) * nf);
+        if (!w->F[k]) return -1;
+    }
+    w->prod = (double*)malloc(sizeof(double) * nf);
+    return w->prod ? 0 : -1;
+}
+
+static void work_free(Work* w) {
+    float* fl[] = {w->s, w->c, w->P, w->Q, w->y0, w->ys, w->y1, w->ca, w->cb, w->cc, w->row, w->cosrow, w->zero};
+    for (size_t i = 0; i < sizeof(fl) / sizeof(fl[0]); ++i) free(fl[i]);
+    for (int k = 0; k < 7; ++k) free(w->F[k]);
+    free(w->prod);
+}
+
+/* -------------------------------------------------------------------- RHS
+ * env.py:252-256:  theta = fmod(y, 2pi);  dy_i = w_i + (K/N) sum_j a_ij
+ * sin(theta_j - theta_i) + pulse_i.  Restated with the exact identity
+ * sin(tj - ti) = s_j c_i - c_j s_i:
+ *   P_i = sum_j a_ij s_j,  Q_i = sum_j a_ij c_j   (fmaf chain, j ascending, from +0)
+ *   coup_i = fmaf(c_i, P_i, -(s_i*Q_i));  f_i = fmaf(kn, coup_i, w_i) + pulse_i
+ */
+static void rhs(const OCtx* o, Work* w, const float* y, const float* omega, const float* pulse, float* f) {
+    const int N = o->N;
+    for (int j = 0; j < N; ++j) {
+        float th = kdm_fmod2pi(y[j]);
+        kdm_sincosf(th, &w->s[j], &w->c[j]);
+    }
+    enum { IB = 256 };
+    for (int ib = 0; ib < N; ib += IB) {
+        int ie = ib + IB < N ? ib + IB : N;
+        float Pb[IB], Qb[IB];
+        for (int i = ib; i < ie; ++i) { Pb[i - ib] = 0.0f; Qb[i - ib] = 0.0f; }
+        for (int j = 0; j < N; ++j) {
+            const float sj = w->s[j], cj = w->c[j];
+            const float* a = o->alphaT + (size_t)j * N;
+            for (int i = ib; i < ie; ++i) {
+                Pb[i - ib] = fmaf(sj, a[i], Pb[i - ib]);
+                Qb[i - ib] = fmaf(cj, a[i], Qb[i - ib]);
+            }
+        }
+        for (int i = ib; i < ie; ++i) { w->P[i] = Pb[i - ib]; w->Q[i] = Qb[i - ib]; }
+    }
+    const float kn = o->cfg.kn;
+    for (int i = 0; i < N; ++i) {
+        float t = w->s[i] * w->Q[i];
+        float coup = fmaf(w->c[i], w->P[i], -t);
+        f[i] = fmaf(kn, coup, omega[i]) + pulse[i];
+    }
+}
+
+/* LFP of one saved row.  naive: mean(cos(row)) in fp32 (env.py:396-401);
+ * gaussian: sum_r mean(cos(row) * g_r) in fp64 (env.py:404-412). */
+static void lfp_row(const OCtx* o, Work* w, const float* row, const double* g_rec, float* naive, double* rec) {
+    const int N = o->N;
+    for (int j = 0; j < N; ++j) w->cosrow[j] = kdm_cosf(row[j]);
+    float m = oracle_r64_f32(w->cosrow, N) / (float)N;
+    *naive = m;
+    if (o->cfg.rec_kernel == KURA_REC_GAUSSIAN) {
+        double acc = 0.0;
+        for (int r = 0; r < o->cfg.n_rec; ++r) {
+            const double* g = g_rec + (size_t)r * N;
+            for (int j = 0; j < N; ++j) w->prod[j] = (double)w->cosrow[j] * g[j];
+            acc = acc + oracle_r64_f64(w->prod, N) / (double)N;
+        }
+        *rec = acc;
+    } else {
+        *rec = (double)m;
+    }
+}
+
+/* Save sink: which rows of a solve produce LFP samples and where they go. */
+typedef struct {
+    float* rows;          /* optional full rows (n*N) */
+    float* lfp_naive;     /* per row index, optional */
+    double* lfp_rec;
+    int lfp_from, lfp_to; /* compute LFP for row indices in [from, to) */
+    const double* g_rec;
+} Sink;
+
+typedef struct { int64_t rhs, steps, rejected, flags; } Stats;
+
+/* One diffeqsolve over the save grid g, starting at y_start (N floats).
+ * On return y_start holds ys[-1]. */
+static void solve(const OCtx* o, Work* w, const Grid* g, float* y_start, const float* omega, const float* pulse,
+                  Sink* sink, Stats* st) {
+    const int N = o->N;
+    const KuraConfig* cfg = &o->cfg;
+    const int n = g->n;
+    if (n <= 0) return;
+    float* y0 = w->y0;
+    memcpy(y0, y_start, sizeof(float) * N);
+    if (n == 1) {  /* t0 == t1: ys = [y0] */
+        if (sink->rows) memcpy(sink->rows, y0, sizeof(float) * N);
+        if (0 >= sink->lfp_from && 0 < sink->lfp_to)
+            lfp_row(o, w, y0, sink->g_rec, &sink->lfp_naive[0], &sink->lfp_rec[0]);
+        return;
+    }
+    const float t0 = (float)grid_at(g, 0);
+    const float t1 = (float)grid_at(g, n - 1);
+    float tprev = t0;
+    float tnext = fminf(t0 + cfg->dt0, t1);
+    rhs(o, w, y0, omega, pulse, w->F[0]);
+    st->rhs += 1;
+    int si = 0;
+    int64_t nsteps = 0;
+    float* const* F = w->F;
+    while (tprev < t1) {
+        if (nsteps >= cfg->max_steps) { st->flags |= 1; break; }
+        ++nsteps;
+        const float h = tnext - tprev;
+        /* stages 2..7: ys = y0 + chain(a_ij * k_j), k_j = h*F[j] */
+        for (int s = 1; s <= 6; ++s) {
+            for (int i = 0; i < N; ++i) {
+                float k0 = h * F[0][i], acc;
+                switch (s) {
+                    case 1: acc = A21 * k0; break;
+                    case 2: acc = A31 * k0; acc = fmaf(A32, h * F[1][i], acc); break;
+                    case 3:
+                        acc = A41 * k0; acc = fmaf(A42, h * F[1][i], acc); acc = fmaf(A43, h * F[2][i], acc);
+                        break;
+                    case 4:
+                        acc = A51 * k0; acc = fmaf(A52, h * F[1][i], acc); acc = fmaf(A53, h * F[2][i], acc);
+                        acc = fmaf(A54, h * F[3][i], acc);
+                        break;
+                    case 5:
+                        acc = A61 * k0; acc = fmaf(A62, h * F[1][i], acc); acc = fmaf(A63, h * F[2][i], acc);
+                        acc = fmaf(A64, h * F[3][i], acc); acc = fmaf(A65, h * F[4][i], acc);
+                        break;
+                    default:
+                        acc = A71 * k0; acc = fmaf(A73, h * F[2][i], acc); acc = fmaf(A74, h * F[3][i], acc);
+                        acc = fmaf(A75, h * F[4][i], acc); acc = fmaf(A76, h * F[5][i], acc);
+                        break;
+                }
+                w->ys[i] = y0[i] + acc;
+            }
+            if (s == 6) memcpy(w->y1, w->ys, sizeof(float) * N);
+            rhs(o, w, w->ys, omega, pulse, F[s]);
+            st->rhs += 1;
+        }
+        /* error estimate and RMS norm */
+        for (int i = 0; i < N; ++i) {
+            float e = E1 * (h * F[0][i]);
+            e = fmaf(E3, h * F[2][i], e);
+            e = fmaf(E4, h * F[3][i], e);
+            e = fmaf(E5, h * F[4][i], e);
+            e = fmaf(E6, h * F[5][i], e);
+            e = fmaf(E7, h * F[6][i], e);
+            float a0 = fabsf(y0[i]), a1 = fabsf(w->y1[i]);
+            float m = a0 > a1 ? a0 : a1;
+            float den = cfg->atol + m * cfg->rtol;
+            float q = e / den;
+            w->cosrow[i] = q * q; /* scratch */
+        }
+        float mean = oracle_r64_f32(w->cosrow, N) / (float)N;
+        float err = sqrtf(mean);
+        int keep = err < 1.0f;
+        float fac = 0.9f * kdm_inv_fifth_root(err);
+        float fmin = keep ? 1.0f : 0.2f;
+        fac = fac > fmin ? fac : fmin;   /* jnp.clip = min(max(x, lo), hi) */
+        fac = fac < 10.0f ? fac : 10.0f;
+        const float dtn = h * fac;
+        if (keep) {
+            /* dense output coefficients (FourthOrderPolynomialInterpolation) */
+            for (int i = 0; i < N; ++i) {
+                float k0 = h * F[0][i], k6 = h * F[6][i];
+                float acc = M1 * k0;
+                acc = fmaf(M3, h * F[2][i], acc);
+                acc = fmaf(M4, h * F[3][i], acc);
+                acc = fmaf(M5, h * F[4][i], acc);
+                acc = fmaf(M6, h * F[5][i], acc);
+                acc = fmaf(M7, k6, acc);
+                float ym = y0[i] + acc;
+                float yy0 = y0[i], yy1 = w->y1[i];
+                w->ca[i] = ((2.0f * (k6 - k0)) - (8.0f * (yy1 + yy0))) + (16.0f * ym);
+                w->cb[i] = ((((5.0f * k0) - (3.0f * k6)) + (18.0f * yy0)) + (14.0f * yy1)) - (32.0f * ym);
+                w->cc[i] = (((k6 - (4.0f * k0)) - (11.0f * yy0)) - (5.0f * yy1)) + (16.0f * ym);
+            }
+            while (si < n) {
+                const float ts = (float)grid_at(g, si);
+                if (!(ts <= tnext)) break;
+                const float th = (ts - tprev) / (tnext - tprev);
+                for (int i = 0; i < N; ++i) {
+                    float k0 = h * F[0][i];
+                    float v = w->ca[i] * th + w->cb[i];
+                    v = v * th + w->cc[i];
+                    v = v * th + k0;
+                    v = v * th + y0[i];
+                    w->row[i] = v;
+                }
+                if (sink->rows) memcpy(sink->rows + (size_t)si * N, w->row, sizeof(float) * N);
+                if (si >= sink->lfp_from && si < sink->lfp_to)
+                    lfp_row(o, w, w->row, sink->g_rec, &sink->lfp_naive[si - sink->lfp_from],
+                            &sink->lfp_rec[si - sink->lfp_from]);
+                if (si == n - 1) memcpy(y_start, w->row, sizeof(float) * N);
+                ++si;
+            }
+            memcpy(y0, w->y1, sizeof(float) * N);
+            memcpy(F[0], F[6], sizeof(float) * N);
+            tprev = tnext;
+        } else {
+            st->rejected += 1;
+        }
+        st->steps += 1;
+        /* next_t0 + dt; tprev = min(tprev, t1); _clip_to_end */
+        float tn = tprev + dtn;
+        tprev = fminf(tprev, t1);
+        if (tn > t1 - 1e-6f) tn = keep ? t1 : tprev + 0.5f * (t1 - tprev);
+        tnext = tn;
+    }
+    if (!(tprev < t1) && si < n) st->flags |= 4; /* unreachable: grid not fully saved */
+    for (int i = 0; i < N; ++i)
+        if (y_start[i] != y_start[i]) { st->flags |= 2; break; }
+}
+
+/* ----------------------------------------------------------------- rewards */
+static double bbpow(const KuraConfig* cfg, const double* x, const double* ctab, const double* stab) {
+    const int W = cfg->window;
+    double bb = 0.0;
+    for (int b = 0; b < cfg->n_bins; ++b) {
+        double re = r64_dot_f64(x, ctab + (size_t)b * W, W);
+        double im = r64_dot_f64(x, stab + (size_t)b * W, W);
+        double pr = re / (double)W, pi = im / (double)W;
+        double p = (pr * pr + pi * pi) * 2.0;
+        bb = bb + p;
+    }
+    return bb;
+}
+
+/* scipy.signal.lfilter direct form II transposed, 5 taps (order-2 band-pass),
+ * scipy/signal/_lfilter.c.in ordering, no contraction. */
+static void lfilter5(const double* b, const double* a, const double* x, double* y, int n, double* z) {
+    for (int k = 0; k < n; ++k) {
+        double xn = x[k];
+        double yn = z[0] + b[0] * xn;
+        z[0] = (z[1] + xn * b[1]) - yn * a[1];
+        z[1] = (z[2] + xn * b[2]) - yn * a[2];
+        z[2] = (z[3] + xn * b[3]) - yn * a[3];
+        z[3] = xn * b[4] - yn * a[4];
+        y[k] = yn;
+    }
+}
+
+/* filtfilt(b, a, x) with padtype='odd', padlen=cfg->padlen, method='pad'.
+ * ext and tmp must hold W + 2*padlen doubles.  Returns filtered[-1] - mean. */
+static double filtfilt_last_dev(const KuraConfig* cfg, const double* x, double* ext, double* tmp) {
+    const int W = cfg->window, p = cfg->padlen, L = W + 2 * p;
+    for (int i = 0; i < p; ++i) ext[i] = 2.0 * x[0] - x[p - i];
+    for (int i = 0; i < W; ++i) ext[p + i] = x[i];
+    for (int i = 0; i < p; ++i) ext[p + W + i] = 2.0 * x[W - 1] - x[W - 2 - i];
+    double z[4];
+    for (int i = 0; i < 4; ++i) z[i] = cfg->bw_zi[i] * ext[0];
+    lfilter5(cfg->bw_b, cfg->bw_a, ext, tmp, L, z);
+    /* backward pass on the reversed output */
+    for (int i = 0; i < L; ++i) ext[i] = tmp[L - 1 - i];
+    for (int i = 0; i < 4; ++i) z[i] = cfg->bw_zi[i] * ext[0];
+    lfilter5(cfg->bw_b, cfg->bw_a, ext, tmp, L, z);
+    /* filtered[i] = tmp[L-1-(p+i)], i in [0, W) */
+    for (int i = 0; i < W; ++i) ext[i] = tmp[L - 1 - p - i];
+    double mean = oracle_r64_f64(ext, W) / (double)W;
+    return ext[W - 1] - mean;
+}
+
+double oracle_reward(const KuraConfig* cfg, const double* x, double u0, const double* ctab, const double* stab) {
+    double au = fabs(u0);
+    if (cfg->reward_kind == KURA_R_BBPOW) {
+        double r1 = 1e4 * bbpow(cfg, x, ctab, stab);
+        return -r1 - 1e-2 * au;
+    } else if (cfg->reward_kind == KURA_R_BBPOW_THR) {
+        double bb = 1e4 * bbpow(cfg, x, ctab, stab);
+        double r1 = bb > 20.0 ? 5.0 : 0.0;
+        return -r1 - au;
+    } else {
+        const int L = cfg->window + 2 * cfg->padlen;
+        double* ext = (double*)malloc(sizeof(double) * L);
+        double* tmp = (double*)malloc(sizeof(double) * L);
+        double d = filtfilt_last_dev(cfg, x, ext, tmp);
+        free(ext);
+        free(tmp);
+        double r1 = 1e3 * (d * d);
+        return -r1 - 1e-2 * au;
+    }
+}
+
+/* ------------------------------------------------------------- env calls */
+static double rescale_action(const KuraConfig* c, float a) {
+    double x = c->act_lo, y = c->act_hi, z = c->dbs_lo, k = c->dbs_hi;
+    return z + ((k - z) * ((double)a - x)) / (y - x);
+}
+
+/* reset(): transient solve from theta0 over arange(0, transient_len, dt);
+ * window = last W of LFP(rows[:-1]).  Arrays are B-major. */
+int oracle_reset(void* ctx, int B, const float* omega, const double* g_rec, const float* theta0, float* y,
+                 double* t, int32_t* step, double* ring, int32_t* wpos, float* obs, int64_t* stats_out) {
+    OCtx* o = (OCtx*)ctx;
+    const KuraConfig* cfg = &o->cfg;
+    const int N = o->N, W = cfg->window;
+    int rc = 0;
+    int64_t agg[4] = {0, 0, 0, 0};
+#pragma omp parallel reduction(| : rc)
+    {
+        Work w;
+        float* lf = (float*)malloc(sizeof(float) * W);
+        double* lr = (double*)malloc(sizeof(double) * W);
+        if (work_alloc(&w, N) || !lf || !lr) rc |= 1;
+#pragma omp for schedule(dynamic, 1)
+        for (int b = 0; b < B; ++b) {
+            if (rc) continue;
+            Grid g = arange(0.0, cfg->transient_len, cfg->dt);
+            float* yb = y + (size_t)b * N;
+            memcpy(yb, theta0 + (size_t)b * N, sizeof(float) * N);
+            Stats st = {0, 0, 0, 0};
+            Sink sk = {NULL, lf, lr, g.n - 1 - W, g.n - 1, g_rec + (size_t)b * cfg->n_rec * N};
+            solve(o, &w, &g, yb, omega + (size_t)b * N, w.zero, &sk, &st);
+            t[b] = grid_at(&g, g.n - 1);
+            step[b] = 0;
+            for (int i = 0; i < W; ++i) ring[(size_t)b * W + i] = lr[i];
+            wpos[b] = 0;
+            if (obs)
+                for (int i = 0; i < W; ++i) obs[(size_t)b * W + i] = (float)lr[i];
+#pragma omp critical
+            {
+                agg[0] = st.rhs > agg[0] ? st.rhs : agg[0];
+                agg[1] += st.steps;
+                agg[2] += st.rejected;
+                agg[3] |= st.flags;
+            }
+        }
+        work_free(&w);
+        free(lf);
+        free(lr);
+    }
+    if (stats_out) memcpy(stats_out, agg, sizeof(agg));
+    return rc ? KURA_E_NOMEM : KURA_OK;
+}
+
+/* step(): env.py:415-454 for B envs.  State arrays (y, t, step, ring, wpos)
+ * are updated in place; outputs are B-major. */
+int oracle_step(void* ctx, int B, const float* omega, const double* g_stim, const double* g_rec,
+                const double* ctab, const double* stab, const float* action, float* y, double* t,
+                int32_t* step, double* ring, int32_t* wpos, float* obs, double* reward, uint8_t* done,
+                float* lfp_true, double* lfp_rec, int32_t* nsamp, int64_t* stats_out) {
+    OCtx* o = (OCtx*)ctx;
+    const KuraConfig* cfg = &o->cfg;
+    const int N = o->N, W = cfg->window, NE = cfg->n_elec;
+    int rc = 0;
+    int64_t agg[4] = {0, 0, 0, 0};
+#pragma omp parallel reduction(| : rc)
+    {
+        Work w;
+        float* pulse = (float*)malloc(sizeof(float) * N);
+        double* x = (double*)malloc(sizeof(double) * W);
+        if (work_alloc(&w, N) || !pulse || !x) rc |= 1;
+#pragma omp for schedule(dynamic, 1)
+        for (int b = 0; b < B; ++b) {
+            if (rc) continue;
+            Stats st = {0, 0, 0, 0};
+            double u[16];
+            for (int e = 0; e < NE && e < 16; ++e) u[e] = rescale_action(cfg, action[(size_t)b * NE + e]);
+            for (int i = 0; i < N; ++i) {
+                double p = 0.0;
+                for (int e = 0; e < NE; ++e) p = p + g_stim[((size_t)b * NE + e) * N + i] * u[e];
+                pulse[i] = (float)p;
+            }
+            float* yb = y + (size_t)b * N;
+            const float* wb = omega + (size_t)b * N;
+            const double* grb = g_rec + (size_t)b * cfg->n_rec * N;
+            float lfN[KURA_S_MAX + 2];
+            double lfR[KURA_S_MAX + 2];
+            /* I: stimulation ON */
+            Grid gI = arange(t[b], t[b] + cfg->width, cfg->dt);
+            Grid gII;
+            int nI = gI.n;
+            if (nI < 2 || nI > KURA_S_MAX) { st.flags |= 8; goto done_env; }
+            {
+                Sink sI = {NULL, lfN, lfR, 0, nI, grb};
+                solve(o, &w, &gI, yb, wb, pulse, &sI, &st);
+                double tm = grid_at(&gI, nI - 1);
+                /* II: stimulation OFF */
+                gII = arange(tm, tm + cfg->pause, cfg->dt);
+                int nII = gII.n;
+                int S = nI + nII - 1;
+                if (nII < 2 || S > KURA_S_MAX) { st.flags |= 8; goto done_env; }
+                lfN[nI] = lfN[nI - 1]; /* ys_II[0] == ys_I[-1] (duplicate row, env.py:440) */
+                lfR[nI] = lfR[nI - 1];
+                Sink sII = {NULL, lfN + nI + 1, lfR + nI + 1, 1, nII - 1, grb};
+                solve(o, &w, &gII, yb, wb, w.zero, &sII, &st);
+                t[b] = grid_at(&gII, nII - 1);
+                /* window: append S records, keep last W (env.py:447-448) */
+                double* rb = ring + (size_t)b * W;
+                int wp = wpos[b];
+                for (int s = 0; s < S; ++s) {
+                    rb[wp] = lfR[s];
+                    wp = wp + 1 == W ? 0 : wp + 1;
+                }
+                wpos[b] = wp;
+                step[b] += 1;
+                done[b] = step[b] >= cfg->episode_steps;
+                for (int i = 0; i < W; ++i) {
+                    int k = wp + i;
+                    x[i] = rb[k >= W ? k - W : k];
+                }
+                reward[b] = oracle_reward(cfg, x, u[0], ctab, stab);
+                if (obs)
+                    for (int i = 0; i < W; ++i) obs[(size_t)b * W + i] = (float)x[i];
+                for (int s = 0; s < KURA_S_MAX; ++s) {
+                    if (lfp_true) lfp_true[(size_t)b * KURA_S_MAX + s] = s < S ? lfN[s] : 0.0f;
+                    if (lfp_rec) lfp_rec[(size_t)b * KURA_S_MAX + s] = s < S ? lfR[s] : 0.0;
+                }
+                nsamp[b] = S;
+            }
+        done_env:
+#pragma omp critical
+            {
+                agg[0] = st.rhs > agg[0] ? st.rhs : agg[0];
+                agg[1] += st.steps;
+                agg[2] += st.rejected;
+                agg[3] |= st.flags;
+            }
+        }
+        work_free(&w);
+        free(pulse);
+        free(x);
+    }
+    if (stats_out) memcpy(stats_out, agg, sizeof(agg));
+    return rc ? KURA_E_NOMEM : KURA_OK;
+}
+
+/* One KuramotoJAX.forward(ts, y0) with explicit save times (used by the
+ * golden-fixture shim that plugs this solver into the reference's
+ * diffrax stub).  rows: n*N output (ys). */
+int oracle_solve_rows(void* ctx, const float* omega, const float* pulse, const double* ts, int n, const float* y0,
+                      float* rows, int64_t* stats_out) {
+    OCtx* o = (OCtx*)ctx;
+    const int N = o->N;
+    Work w;
+    if (work_alloc(&w, N)) return KURA_E_NOMEM;
+    Grid g;
+    g.start = ts[0];
+    g.delta = 0.0;
+    g.n = n;
+    g.vals = ts;
+    float* y = (float*)malloc(sizeof(float) * N);
+    memcpy(y, y0, sizeof(float) * N);
+    Stats st = {0, 0, 0, 0};
+    Sink sk = {rows, NULL, NULL, 0, 0, NULL};
+    solve(o, &w, &g, y, omega, pulse ? pulse : w.zero, &sk, &st);
+    free(y);
+    work_free(&w);
+    if (stats_out) {
+        stats_out[0] = st.rhs;
+        stats_out[1] = st.steps;
+        stats_out[2] = st.rejected;
+        stats_out[3] = st.flags;
+    }
+    return KURA_OK;
+}
+
+/* Exported pieces for unit tests against the GPU. */
+void oracle_rhs(void* ctx, const float* y, const float* omega, const float* pulse, float* f) {
+    OCtx* o = (OCtx*)ctx;
+    Work w;
+    if (work_alloc(&w, o->N)) return;
+    rhs(o, &w, y, omega, pulse, f);
+    work_free(&w);
+}
+
+void oracle_sincos(const float* x, float* s, float* c, int n) {
+    for (int i = 0; i < n; ++i) kdm_sincosf(x[i], &s[i], &c[i]);
+}
+void oracle_fmod2pi(const float* x, float* r, int n) {
+    for (int i = 0; i < n; ++i) r[i] = kdm_fmod2pi(x[i]);
+}
+void oracle_inv_fifth_root(const float* x, float* r, int n) {
+    for (int i = 0; i < n; ++i) r[i] = kdm_inv_fifth_root(x[i]);
+}
+/* sequential fmaf chain GEMM (the MFMA 32x32x2 f32 k-order):
+ * Y[r][i] = fmaf chain over k of X[r][k]*A[i][k], from +0. */
+void oracle_gemm_chain(const float* X, const float* A, float* Y, int M, int N, int K) {
+    for (int r = 0; r < M; ++r)
+        for (int i = 0; i < N; ++i) {
+            float acc = 0.0f;
+            for (int k = 0; k < K; ++k) acc = fmaf(X[(size_t)r * K + k], A[(size_t)i * K + k], acc);
+            Y[(size_t)r * N + i] = acc;
+        }
+}

@@ -1,0 +1,195 @@
+"""ctypes wrapper of the CPU oracle (oracle/libkura_oracle.so).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg -- never by the product package.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+from ctypes import c_double, c_int, c_void_p
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "libkura_oracle.so")
+S_MAX = 32
+
+
+def build(force: bool = False) -> str:
+    if force or not os.path.exists(LIB) or os.path.getmtime(LIB) < os.path.getmtime(os.path.join(HERE, "kura_oracle.c")):
+        subprocess.run(["make", "-C", HERE, "-B" if force else "all"], check=True, capture_output=True)
+    return LIB
+
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is None:
+        build()
+        L = ctypes.CDLL(LIB)
+        L.oracle_create.restype = c_void_p
+        L.oracle_create.argtypes = [c_void_p, c_void_p]
+        L.oracle_destroy.argtypes = [c_void_p]
+        L.oracle_reset.restype = c_int
+        L.oracle_reset.argtypes = [c_void_p, c_int] + [c_void_p] * 10
+        L.oracle_step.restype = c_int
+        L.oracle_step.argtypes = [c_void_p, c_int] + [c_void_p] * 17
+        L.oracle_solve_rows.restype = c_int
+        L.oracle_solve_rows.argtypes = [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p]
+        L.oracle_rhs.argtypes = [c_void_p] * 5
+        L.oracle_reward.restype = c_double
+        L.oracle_reward.argtypes = [c_void_p, c_void_p, c_double, c_void_p, c_void_p]
+        L.oracle_r64_f32.restype = ctypes.c_float
+        L.oracle_r64_f32.argtypes = [c_void_p, c_int]
+        L.oracle_r64_f64.restype = c_double
+        L.oracle_r64_f64.argtypes = [c_void_p, c_int]
+        L.oracle_arange.restype = c_int
+        L.oracle_arange.argtypes = [c_double, c_double, c_double, c_void_p, c_int]
+        for n in ("oracle_sincos",):
+            getattr(L, n).argtypes = [c_void_p, c_void_p, c_void_p, c_int]
+        for n in ("oracle_fmod2pi", "oracle_inv_fifth_root"):
+            getattr(L, n).argtypes = [c_void_p, c_void_p, c_int]
+        L.oracle_gemm_chain.argtypes = [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int]
+        _lib = L
+    return _lib
+
+
+def _p(a):
+    return None if a is None else a.ctypes.data
+
+
+class Oracle:
+    """Mirror of KuraSim on the CPU (same state layout, host arrays)."""
+
+    def __init__(self, cfg, alpha: np.ndarray):
+        self.cfg = cfg
+        self.N, self.B, self.W = cfg.n_osc, cfg.n_envs, cfg.window
+        self._alpha = np.ascontiguousarray(alpha, np.float32)
+        self._ctx = lib().oracle_create(ctypes.byref(cfg), self._alpha.ctypes.data)
+        B, N, W = self.B, self.N, self.W
+        self.y = np.zeros((B, N), np.float32)
+        self.t = np.zeros(B, np.float64)
+        self.step_count = np.zeros(B, np.int32)
+        self.ring = np.zeros((B, W), np.float64)
+        self.wpos = np.zeros(B, np.int32)
+        self.stats = np.zeros(4, np.int64)
+
+    def set_env_params(self, omega, g_stim, g_rec=None):
+        self.omega = np.ascontiguousarray(omega, np.float32)
+        self.g_stim = np.ascontiguousarray(g_stim, np.float64)
+        nr = max(self.cfg.n_rec, 1)
+        self.g_rec = (np.ascontiguousarray(g_rec, np.float64) if g_rec is not None
+                      else np.zeros((self.B, nr, self.N), np.float64))
+
+    def set_spectral(self, ctab, stab):
+        self.ctab = np.ascontiguousarray(ctab, np.float64)
+        self.stab = np.ascontiguousarray(stab, np.float64)
+
+    def reset(self, theta0):
+        th = np.ascontiguousarray(theta0, np.float32)
+        obs = np.zeros((self.B, self.W), np.float32)
+        rc = lib().oracle_reset(self._ctx, self.B, _p(self.omega), _p(self.g_rec), _p(th), _p(self.y), _p(self.t),
+                                _p(self.step_count), _p(self.ring), _p(self.wpos), _p(obs), _p(self.stats))
+        assert rc == 0
+        return obs
+
+    def step(self, action):
+        a = np.ascontiguousarray(action, np.float32)
+        B = self.B
+        out = dict(obs=np.zeros((B, self.W), np.float32), reward=np.zeros(B, np.float64),
+                   done=np.zeros(B, np.uint8), lfp_true=np.zeros((B, S_MAX), np.float32),
+                   lfp_rec=np.zeros((B, S_MAX), np.float64), nsamp=np.zeros(B, np.int32))
+        rc = lib().oracle_step(self._ctx, B, _p(self.omega), _p(self.g_stim), _p(self.g_rec), _p(self.ctab),
+                               _p(self.stab), _p(a), _p(self.y), _p(self.t), _p(self.step_count), _p(self.ring),
+                               _p(self.wpos), _p(out["obs"]), _p(out["reward"]), _p(out["done"]),
+                               _p(out["lfp_true"]), _p(out["lfp_rec"]), _p(out["nsamp"]), _p(self.stats))
+        assert rc == 0
+        return out
+
+    def state(self):
+        return dict(y=self.y.copy(), t=self.t.copy(), step=self.step_count.copy(), ring=self.ring.copy(),
+                    wpos=self.wpos.copy())
+
+    def solve_rows(self, omega, pulse, ts, y0):
+        N = self.N
+        ts = np.ascontiguousarray(ts, np.float64)
+        rows = np.zeros((len(ts), N), np.float32)
+        st = np.zeros(4, np.int64)
+        rc = lib().oracle_solve_rows(self._ctx, _p(np.ascontiguousarray(omega, np.float32)),
+                                     _p(None if pulse is None else np.ascontiguousarray(pulse, np.float32)),
+                                     _p(ts), len(ts), _p(np.ascontiguousarray(y0, np.float32)), _p(rows), _p(st))
+        assert rc == 0
+        return rows, st
+
+    def rhs(self, y, omega, pulse):
+        f = np.zeros(self.N, np.float32)
+        lib().oracle_rhs(self._ctx, _p(np.ascontiguousarray(y, np.float32)), _p(np.ascontiguousarray(omega, np.float32)),
+                         _p(np.ascontiguousarray(pulse, np.float32)), _p(f))
+        return f
+
+    def reward(self, window, u0):
+        return lib().oracle_reward(ctypes.byref(self.cfg), _p(np.ascontiguousarray(window, np.float64)), float(u0),
+                                   _p(self.ctab), _p(self.stab))
+
+    def close(self):
+        if self._ctx:
+            lib().oracle_destroy(self._ctx)
+            self._ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def sincos(x):
+    x = np.ascontiguousarray(x, np.float32)
+    s = np.empty_like(x)
+    c = np.empty_like(x)
+    lib().oracle_sincos(_p(x), _p(s), _p(c), x.size)
+    return s, c
+
+
+def fmod2pi(x):
+    x = np.ascontiguousarray(x, np.float32)
+    r = np.empty_like(x)
+    lib().oracle_fmod2pi(_p(x), _p(r), x.size)
+    return r
+
+
+def inv_fifth_root(x):
+    x = np.ascontiguousarray(x, np.float32)
+    r = np.empty_like(x)
+    lib().oracle_inv_fifth_root(_p(x), _p(r), x.size)
+    return r
+
+
+def gemm_chain(X, A):
+    X = np.ascontiguousarray(X, np.float32)
+    A = np.ascontiguousarray(A, np.float32)
+    M, K = X.shape
+    N = A.shape[0]
+    Y = np.empty((M, N), np.float32)
+    lib().oracle_gemm_chain(_p(X), _p(A), _p(Y), M, N, K)
+    return Y
+
+
+def r64_f32(x):
+    x = np.ascontiguousarray(x, np.float32)
+    return lib().oracle_r64_f32(_p(x), x.size)
+
+
+def r64_f64(x):
+    x = np.ascontiguousarray(x, np.float64)
+    return lib().oracle_r64_f64(_p(x), x.size)
+
+
+def arange(start, stop, step, cap=100000):
+    out = np.empty(cap, np.float64)
+    n = lib().oracle_arange(start, stop, step, _p(out), cap)
+    return out[:n]
