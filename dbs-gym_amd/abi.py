@@ -91,6 +91,9 @@ _SYMBOLS = {
     "kura_get_state": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "kura_set_state": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "kura_get_stats": (c_int, [c_void_p, c_void_p]),
+    "kura_get_stamps": (c_int, [c_void_p, c_void_p]),
+    "kura_selftest_math": (c_int, [c_void_p, c_void_p, c_void_p, c_int]),
+    "kura_selftest_gemm": (c_int, [c_void_p, c_void_p, c_void_p, c_int]),
 }
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))

@@ -33,29 +33,36 @@ typedef float floatx4 __attribute__((ext_vector_type(4)));
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 
 // ---- Dopri5 tableau cast to fp32 (identical constants to the oracle) -------
+// kA[s][j]: stage s input = y0 + chain_j(kA[s][j] * k_j); kE: error weights;
+// kM: dense-output mid-point weights (diffrax _Dopri5Interpolation.c_mid).
 #define KF(x) ((float)(x))
-__constant__ static const float kA21 = KF(1.0 / 5.0);
-__constant__ static const float kA31 = KF(3.0 / 40.0), kA32 = KF(9.0 / 40.0);
-__constant__ static const float kA41 = KF(44.0 / 45.0), kA42 = KF(-56.0 / 15.0), kA43 = KF(32.0 / 9.0);
-__constant__ static const float kA51 = KF(19372.0 / 6561.0), kA52 = KF(-25360.0 / 2187.0),
-                                kA53 = KF(64448.0 / 6561.0), kA54 = KF(-212.0 / 729.0);
-__constant__ static const float kA61 = KF(9017.0 / 3168.0), kA62 = KF(-355.0 / 33.0),
-                                kA63 = KF(46732.0 / 5247.0), kA64 = KF(49.0 / 176.0),
-                                kA65 = KF(-5103.0 / 18656.0);
-__constant__ static const float kA71 = KF(35.0 / 384.0), kA73 = KF(500.0 / 1113.0), kA74 = KF(125.0 / 192.0),
-                                kA75 = KF(-2187.0 / 6784.0), kA76 = KF(11.0 / 84.0);
-__constant__ static const float kE1 = KF(35.0 / 384.0 - 1951.0 / 21600.0),
-                                kE3 = KF(500.0 / 1113.0 - 22642.0 / 50085.0),
-                                kE4 = KF(125.0 / 192.0 - 451.0 / 720.0),
-                                kE5 = KF(-2187.0 / 6784.0 + 12231.0 / 42400.0),
-                                kE6 = KF(11.0 / 84.0 - 649.0 / 6300.0), kE7 = KF(-1.0 / 60.0);
-__constant__ static const float kM1 = KF(6025192743.0 / 30085553152.0 / 2.0),
-                                kM3 = KF(51252292925.0 / 65400821598.0 / 2.0),
-                                kM4 = KF(-2691868925.0 / 45128329728.0 / 2.0),
-                                kM5 = KF(187940372067.0 / 1594534317056.0 / 2.0),
-                                kM6 = KF(-1776094331.0 / 19743644256.0 / 2.0),
-                                kM7 = KF(11237099.0 / 235043384.0 / 2.0);
+__device__ constexpr float kA[7][6] = {
+    {0, 0, 0, 0, 0, 0},
+    {KF(1.0 / 5.0), 0, 0, 0, 0, 0},
+    {KF(3.0 / 40.0), KF(9.0 / 40.0), 0, 0, 0, 0},
+    {KF(44.0 / 45.0), KF(-56.0 / 15.0), KF(32.0 / 9.0), 0, 0, 0},
+    {KF(19372.0 / 6561.0), KF(-25360.0 / 2187.0), KF(64448.0 / 6561.0), KF(-212.0 / 729.0), 0, 0},
+    {KF(9017.0 / 3168.0), KF(-355.0 / 33.0), KF(46732.0 / 5247.0), KF(49.0 / 176.0), KF(-5103.0 / 18656.0), 0},
+    {KF(35.0 / 384.0), 0, KF(500.0 / 1113.0), KF(125.0 / 192.0), KF(-2187.0 / 6784.0), KF(11.0 / 84.0)}};
+__device__ constexpr float kE[7] = {KF(35.0 / 384.0 - 1951.0 / 21600.0), 0,
+                                    KF(500.0 / 1113.0 - 22642.0 / 50085.0), KF(125.0 / 192.0 - 451.0 / 720.0),
+                                    KF(-2187.0 / 6784.0 + 12231.0 / 42400.0), KF(11.0 / 84.0 - 649.0 / 6300.0),
+                                    KF(-1.0 / 60.0)};
+__device__ constexpr float kM[7] = {KF(6025192743.0 / 30085553152.0 / 2.0), 0,
+                                    KF(51252292925.0 / 65400821598.0 / 2.0),
+                                    KF(-2691868925.0 / 45128329728.0 / 2.0),
+                                    KF(187940372067.0 / 1594534317056.0 / 2.0),
+                                    KF(-1776094331.0 / 19743644256.0 / 2.0), KF(11237099.0 / 235043384.0 / 2.0)};
 #undef KF
+// same values, addressable with a runtime stage index (scalar loads)
+__constant__ float cA[7][6] = {
+    {0, 0, 0, 0, 0, 0},
+    {kA[1][0], 0, 0, 0, 0, 0},
+    {kA[2][0], kA[2][1], 0, 0, 0, 0},
+    {kA[3][0], kA[3][1], kA[3][2], 0, 0, 0},
+    {kA[4][0], kA[4][1], kA[4][2], kA[4][3], 0, 0},
+    {kA[5][0], kA[5][1], kA[5][2], kA[5][3], kA[5][4], 0},
+    {kA[6][0], kA[6][1], kA[6][2], kA[6][3], kA[6][4], kA[6][5]}};
 
 // Everything a launch needs, passed by value (kernarg).
 struct DevParams {
@@ -75,18 +82,43 @@ struct DevParams {
     int* step;              // [B]
     double* ring;           // [B][W] observation window ring
     int* wpos;              // [B] next write slot == oldest sample
-    float* F;               // [B][7][N] stage derivatives
-    float* Y0;              // [B][N]
+    float* R;               // [B][N][8] per-oscillator record {y0, f_0 .. f_6} (f_j = RHS at stage j)
     float* Y1;              // [B][N]
     float* pulse;           // [B][N]
     double* scratch;        // [B][W + 2*padlen] * 2 (R2 filtfilt)
     unsigned long long* stats;  // [4]: max rhs, steps, rejected, flags
+    unsigned long long* stamps; // [NWAVES][8] phase cycle counters (KURA_STAMPS builds only)
 };
 
-// LDS index of X[row][k] in MFMA A-fragment order: for k-block kb = k/8 the
-// 64 lanes' 4 consecutive k-steps are 16 contiguous bytes (one ds_read_b128).
+// Diagnostic phase timers (compile with -DKURA_STAMPS): per wave, cycles
+// spent in stage-input / barrier / GEMM / epilogue / barrier / post-step /
+// flag-sync, accumulated with s_memtime and added into p.stamps at the end.
+#ifdef KURA_STAMPS
+#define STAMP_DECL unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}; unsigned long long st_last = __builtin_amdgcn_s_memtime();
+#define STAMP(k) do { unsigned long long n_ = __builtin_amdgcn_s_memtime(); st_acc[k] += n_ - st_last; st_last = n_; } while (0)
+#define STAMP_FLUSH(p) do { if ((threadIdx.x & 63) == 0 && (p).stamps) for (int k_ = 0; k_ < 8; ++k_) atomicAdd(&(p).stamps[(threadIdx.x >> 6) * 8 + k_], st_acc[k_]); } while (0)
+#else
+#define STAMP_DECL
+#define STAMP(k) do { } while (0)
+#define STAMP_FLUSH(p) do { } while (0)
+#endif
+
+// Per-workgroup LDS besides the dynamic 32 x N operand: LFP samples of the
+// current step (one row per env) and the "any env still integrating" flag.
+__shared__ float s_smp_n[E_WG][KURA_S_MAX + 2];
+__shared__ double s_smp_r[E_WG][KURA_S_MAX + 2];
+__shared__ int s_wg_flag;
+
+// LDS index of X[row][k] in MFMA A-fragment order: for k-block kb = k/8,
+// lane (row + 32*(k&1)) holds its 4 consecutive k-steps in 16 contiguous
+// bytes (one ds_read_b128).  Each 32-lane half is followed by a 16-byte pad
+// (block = 264 floats), which makes the row-strided epilogue reads and the
+// R64-layout stage-input writes bank-conflict free.
+#define XS_HALF 132
+#define XS_BLOCK 264
+__host__ __device__ constexpr int xs_floats(int N) { return (N / 8) * XS_BLOCK; }
 __device__ __forceinline__ int xs_idx(int row, int k) {
-    return (((k >> 3) * 64 + row + 32 * (k & 1)) << 2) + ((k >> 1) & 3);
+    return (k >> 3) * XS_BLOCK + (k & 1) * XS_HALF + (row << 2) + ((k >> 1) & 3);
 }
 
 __device__ __forceinline__ float wave_sum_f32(float v) {
@@ -127,126 +159,157 @@ struct Ctl {
 
 // ---------------------------------------------------------------- GEMM ----
 // acc[t] (32 x 32 tile, columns jt = wave*TPW + t) = X (LDS) x B-fragments.
+// alpha fragments are read as global (addrspace 1) 16-byte loads so the
+// compiler can count vmcnt precisely; two buffers give a prefetch distance of
+// one k-block (16 MFMAs of this wave + the partner wave's) per load.
+typedef const __attribute__((address_space(1))) floatx4 gfloatx4;
+
 template <int TPW>
 __device__ __forceinline__ void coupling_gemm(const float* __restrict__ Xs, const float* __restrict__ alpha_sw,
-                                              int N, floatx16 (&acc)[TPW]) {
+                                              floatx16 (&acc)[TPW]) {
+    constexpr int N = TPW * 256;
+    constexpr int NK8 = N / 8;
+    constexpr int TSTRIDE = NK8 * 64;  // floatx4 per column tile
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int NK8 = N >> 3;
 #pragma unroll
     for (int t = 0; t < TPW; ++t)
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[t][r] = 0.0f;
-    const floatx4* xs4 = reinterpret_cast<const floatx4*>(Xs);
-    const floatx4* bp[TPW];
+    // lane l reads floats [kb*XS_BLOCK + (l>>5)*XS_HALF + (l&31)*4, +4)
+    const floatx4* xs4 = reinterpret_cast<const floatx4*>(Xs + (lane >> 5) * XS_HALF + (lane & 31) * 4);
+    gfloatx4* bp = (gfloatx4*)(alpha_sw) + (size_t)(wave * TPW) * TSTRIDE + lane;
+    floatx4 b0[TPW], b1[TPW];
 #pragma unroll
-    for (int t = 0; t < TPW; ++t)
-        bp[t] = reinterpret_cast<const floatx4*>(alpha_sw) + ((size_t)(wave * TPW + t) * NK8) * 64 + lane;
-    floatx4 bcur[TPW], bnxt[TPW];
-#pragma unroll
-    for (int t = 0; t < TPW; ++t) bcur[t] = bp[t][0];
-    for (int kb = 0; kb < NK8; ++kb) {
-        if (kb + 1 < NK8) {
-#pragma unroll
-            for (int t = 0; t < TPW; ++t) bnxt[t] = bp[t][(size_t)(kb + 1) * 64];
-        }
-        floatx4 a = xs4[kb * 64 + lane];
+    for (int t = 0; t < TPW; ++t) {
+        b0[t] = bp[t * TSTRIDE];
+        b1[t] = bp[t * TSTRIDE + 64];
+    }
+#pragma unroll 1
+    for (int kb = 0; kb < NK8; kb += 2) {
+        floatx4 a = xs4[kb * (XS_BLOCK / 4)];
 #pragma unroll
         for (int s = 0; s < 4; ++s)
 #pragma unroll
             for (int t = 0; t < TPW; ++t)
-                acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s], bcur[t][s], acc[t], 0, 0, 0);
+                acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s], b0[t][s], acc[t], 0, 0, 0);
+        // unconditional (clamped) prefetch keeps the vmcnt bookkeeping exact
+        const int k2 = kb + 2 < NK8 ? kb + 2 : NK8 - 1;
 #pragma unroll
-        for (int t = 0; t < TPW; ++t) bcur[t] = bnxt[t];
+        for (int t = 0; t < TPW; ++t) b0[t] = bp[t * TSTRIDE + k2 * 64];
+        a = xs4[(kb + 1) * (XS_BLOCK / 4)];
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+            for (int t = 0; t < TPW; ++t)
+                acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s], b1[t][s], acc[t], 0, 0, 0);
+        const int k3 = kb + 3 < NK8 ? kb + 3 : NK8 - 1;
+#pragma unroll
+        for (int t = 0; t < TPW; ++t) b1[t] = bp[t * TSTRIDE + k3 * 64];
     }
 }
 
-// f = fmaf(kn, fmaf(c, P, -(s*Q)), omega) + pulse  ->  F[env][stage][i]
+// MFMA-layout element ownership: lane holds, for each of its TPW column tiles,
+// accumulator rows q = 0..7 (sin rows of env e(q)) and q+8 (cos rows of the
+// same env).  e(q) = (q&3) + 8(q>>2) + 4(lane>>5); column i = 32*jt + (lane&31).
+__device__ __forceinline__ int mfma_env(int q, int lane) { return (q & 3) + 8 * (q >> 2) + 4 * (lane >> 5); }
+
+// omega and pulse of the lane's MFMA-layout elements, fetched at the start of
+// the GEMM so their latency hides under the K loop.
 template <int TPW>
-__device__ __forceinline__ void coupling_epilogue(const DevParams& p, const float* __restrict__ Xs,
-                                                  const floatx16 (&acc)[TPW], int env_base, int stage) {
+struct EpiConst {
+    float w[TPW][8];
+    float u[TPW][8];
+};
+
+template <int TPW>
+__device__ __forceinline__ void load_epi_const(const DevParams& p, int env_base, bool pulse_on,
+                                               EpiConst<TPW>& k) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int N = p.N;
-    const int h = lane >> 5;
+    constexpr int N = TPW * 256;
 #pragma unroll
     for (int t = 0; t < TPW; ++t) {
         const int i = 32 * (wave * TPW + t) + (lane & 31);
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
-            const int e = (q & 3) + 8 * (q >> 2) + 4 * h;
-            const int env = env_base + e;
-            if (env >= p.B) continue;
-            const float P = acc[t][q], Q = acc[t][q + 8];
-            const float s = Xs[xs_idx(e, i)], c = Xs[xs_idx(16 + e, i)];
+            int env = env_base + mfma_env(q, lane);
+            env = env < p.B ? env : p.B - 1;  // padded rows: any valid address
             const size_t o = (size_t)env * N + i;
-            const float tq = s * Q;
-            const float coup = __builtin_fmaf(c, P, -tq);
-            const float f = __builtin_fmaf(p.kn, coup, p.omega[o]) + p.pulse[o];
-            p.F[((size_t)env * 7 + stage) * N + i] = f;
+            k.w[t][q] = p.omega[o];
+            k.u[t][q] = pulse_on ? p.pulse[o] : 0.0f;  // pulse = 0 while OFF (env.py:434)
+        }
+    }
+}
+
+// f = fmaf(kn, fmaf(c, P, -(s*Q)), omega) + pulse  ->  R[env][i][1 + stage]
+template <int TPW>
+__device__ __forceinline__ void coupling_epilogue(const DevParams& p, const float* __restrict__ Xs,
+                                                  const floatx16 (&acc)[TPW], const EpiConst<TPW>& kc,
+                                                  int env_base, int stage) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    constexpr int N = TPW * 256;
+#pragma unroll
+    for (int t = 0; t < TPW; ++t) {
+        const int i = 32 * (wave * TPW + t) + (lane & 31);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const int e = mfma_env(q, lane);
+            const int env = env_base + e;
+            const float P = acc[t][q], Q = acc[t][q + 8];
+            const float sn = Xs[xs_idx(e, i)], cs = Xs[xs_idx(16 + e, i)];
+            const float tq = sn * Q;
+            const float coup = __builtin_fmaf(cs, P, -tq);
+            const float f = __builtin_fmaf(p.kn, coup, kc.w[t][q]) + kc.u[t][q];
+            if (env < p.B) p.R[((size_t)env * N + i) * 8 + 1 + stage] = f;
         }
     }
 }
 
 // ------------------------------------------------------------ R64 stages ---
-// Stage input ys = y0 + chain(a_s,j * h*F_j), then theta = fmod(ys, 2pi) and
-// sin/cos into the LDS operand.  Stage 0 is the solve's initial RHS at y0.
+// Stage input ys = y0 + chain_j(A[s][j] * h*f_j) (zero coefficients skipped,
+// as in the oracle), theta = fmod(ys, 2pi) and sin/cos into the LDS operand.
+// Stage 0 is the solve's initial RHS at y0.  Each element's record is read
+// with one or two 16-byte loads; 8 elements are in flight per batch.
 template <int EPL>
 __device__ __forceinline__ void stage_input(const DevParams& p, float* Xs, const Ctl (&ctl)[ENVS_PER_WAVE],
                                             int env_base, int s) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int N = p.N;
-#pragma unroll
+    constexpr int N = EPL * 64;
+    constexpr int CH = EPL < 8 ? EPL : 8;
+#pragma unroll 1
     for (int ee = 0; ee < ENVS_PER_WAVE; ++ee) {
         const int e = wave * ENVS_PER_WAVE + ee;
         const int env = env_base + e;
         if (env >= p.B || !ctl[ee].active) continue;
         const float h = ctl[ee].h;
-        const float* Fe = p.F + (size_t)env * 7 * N;
-        const float* y0 = p.Y0 + (size_t)env * N;
-#pragma unroll 4
-        for (int m = 0; m < EPL; ++m) {
-            const int i = lane + 64 * m;
-            float ys;
-            if (s == 0) {
-                ys = y0[i];
-            } else {
-                const float k0 = h * Fe[i];
-                float acc;
-                switch (s) {
-                    case 1: acc = kA21 * k0; break;
-                    case 2: acc = kA31 * k0; acc = __builtin_fmaf(kA32, h * Fe[N + i], acc); break;
-                    case 3:
-                        acc = kA41 * k0;
-                        acc = __builtin_fmaf(kA42, h * Fe[N + i], acc);
-                        acc = __builtin_fmaf(kA43, h * Fe[2 * N + i], acc);
-                        break;
-                    case 4:
-                        acc = kA51 * k0;
-                        acc = __builtin_fmaf(kA52, h * Fe[N + i], acc);
-                        acc = __builtin_fmaf(kA53, h * Fe[2 * N + i], acc);
-                        acc = __builtin_fmaf(kA54, h * Fe[3 * N + i], acc);
-                        break;
-                    case 5:
-                        acc = kA61 * k0;
-                        acc = __builtin_fmaf(kA62, h * Fe[N + i], acc);
-                        acc = __builtin_fmaf(kA63, h * Fe[2 * N + i], acc);
-                        acc = __builtin_fmaf(kA64, h * Fe[3 * N + i], acc);
-                        acc = __builtin_fmaf(kA65, h * Fe[4 * N + i], acc);
-                        break;
-                    default:
-                        acc = kA71 * k0;
-                        acc = __builtin_fmaf(kA73, h * Fe[2 * N + i], acc);
-                        acc = __builtin_fmaf(kA74, h * Fe[3 * N + i], acc);
-                        acc = __builtin_fmaf(kA75, h * Fe[4 * N + i], acc);
-                        acc = __builtin_fmaf(kA76, h * Fe[5 * N + i], acc);
-                        break;
-                }
-                ys = y0[i] + acc;
-                if (s == 6) p.Y1[(size_t)env * N + i] = ys;
+        const floatx4* rec = reinterpret_cast<const floatx4*>(p.R + (size_t)env * N * 8) + 2 * lane;
+#pragma unroll 1
+        for (int m0 = 0; m0 < EPL; m0 += CH) {
+            floatx4 lo[CH], hi[CH];
+#pragma unroll
+            for (int m = 0; m < CH; ++m) {
+                lo[m] = rec[2 * 64 * (m0 + m)];
+                if (s >= 4) hi[m] = rec[2 * 64 * (m0 + m) + 1];
             }
-            float sn, cs;
-            kdm_sincosf(kdm_fmod2pi(ys), &sn, &cs);
-            Xs[xs_idx(e, i)] = sn;
-            Xs[xs_idx(16 + e, i)] = cs;
+#pragma unroll
+            for (int m = 0; m < CH; ++m) {
+                const int i = lane + 64 * (m0 + m);
+                // record: lo = {y0, f0, f1, f2}, hi = {f3, f4, f5, f6}
+                float ys = lo[m][0];
+                if (s > 0) {
+                    float acc = cA[s][0] * (h * lo[m][1]);
+                    if (s > 1 && cA[s][1] != 0.0f) acc = __builtin_fmaf(cA[s][1], h * lo[m][2], acc);
+                    if (s > 2) acc = __builtin_fmaf(cA[s][2], h * lo[m][3], acc);
+                    if (s > 3) acc = __builtin_fmaf(cA[s][3], h * hi[m][0], acc);
+                    if (s > 4) acc = __builtin_fmaf(cA[s][4], h * hi[m][1], acc);
+                    if (s > 5) acc = __builtin_fmaf(cA[s][5], h * hi[m][2], acc);
+                    ys = lo[m][0] + acc;
+                    if (s == 6) p.Y1[(size_t)env * N + i] = ys;
+                }
+                float sn, cs;
+                kdm_sincosf(kdm_fmod2pi(ys), &sn, &cs);
+                Xs[xs_idx(e, i)] = sn;
+                Xs[xs_idx(16 + e, i)] = cs;
+            }
         }
     }
 }
@@ -256,7 +319,7 @@ template <int EPL>
 __device__ __forceinline__ void lfp_of_row(const DevParams& p, int env, const float (&row)[EPL], float* naive,
                                            double* rec) {
     const int lane = threadIdx.x & 63;
-    const int N = p.N;
+    constexpr int N = EPL * 64;
     float cr[EPL];
     float part = 0.0f;
 #pragma unroll
@@ -282,33 +345,50 @@ __device__ __forceinline__ void lfp_of_row(const DevParams& p, int env, const fl
 }
 
 // After the 7th stage: error norm, accept/reject, dense-output saves, FSAL.
-// smp_n/smp_r: LDS sample buffers of this env; ring_dst: if non-null, samples
-// go straight to the observation ring (reset transient).
+// One pass over the env's lane elements reads each record (two 16-byte loads)
+// and y1, forms the scaled error and the dense-output coefficients; then the
+// R64 reduction decides acceptance and the saves are evaluated from registers.
 template <int EPL>
-__device__ __forceinline__ void post_step(const DevParams& p, Ctl& c, int env, float* smp_n, double* smp_r,
-                                          double* ring_dst) {
+__device__ __forceinline__ void post_step(const DevParams& p, Ctl& c, int env, int e, bool to_ring) {
     const int lane = threadIdx.x & 63;
-    const int N = p.N;
+    constexpr int N = EPL * 64;
     const float h = c.h;
-    float* Fe = p.F + (size_t)env * 7 * N;
-    float* y0p = p.Y0 + (size_t)env * N;
-    const float* y1p = p.Y1 + (size_t)env * N;
-    // error estimate + RMS norm (R64)
+    floatx4* rec = reinterpret_cast<floatx4*>(p.R + (size_t)env * N * 8) + 2 * lane;
+    const float* y1p = p.Y1 + (size_t)env * N + lane;
+    float ca[EPL], cb[EPL], cc[EPL], k0v[EPL], y0v[EPL];
     float part = 0.0f;
-#pragma unroll 4
+#pragma unroll
     for (int m = 0; m < EPL; ++m) {
-        const int i = lane + 64 * m;
-        float e = kE1 * (h * Fe[i]);
-        e = __builtin_fmaf(kE3, h * Fe[2 * N + i], e);
-        e = __builtin_fmaf(kE4, h * Fe[3 * N + i], e);
-        e = __builtin_fmaf(kE5, h * Fe[4 * N + i], e);
-        e = __builtin_fmaf(kE6, h * Fe[5 * N + i], e);
-        e = __builtin_fmaf(kE7, h * Fe[6 * N + i], e);
-        const float a0 = fabsf(y0p[i]), a1 = fabsf(y1p[i]);
+        const floatx4 lo = rec[2 * 64 * m], hi = rec[2 * 64 * m + 1];
+        const float yy1 = y1p[64 * m];
+        const float yy0 = lo[0];
+        const float k0 = h * lo[1], k2 = h * lo[3], k3 = h * hi[0], k4 = h * hi[1], k5 = h * hi[2],
+                    k6 = h * hi[3];
+        // error estimate (b_sol - b_embedded) and its scaled square
+        float er = kE[0] * k0;
+        er = __builtin_fmaf(kE[2], k2, er);
+        er = __builtin_fmaf(kE[3], k3, er);
+        er = __builtin_fmaf(kE[4], k4, er);
+        er = __builtin_fmaf(kE[5], k5, er);
+        er = __builtin_fmaf(kE[6], k6, er);
+        const float a0 = fabsf(yy0), a1 = fabsf(yy1);
         const float mx = a0 > a1 ? a0 : a1;
         const float den = p.atol + mx * p.rtol;
-        const float q = e / den;
-        part = part + q * q;
+        const float qe = er / den;
+        part = part + qe * qe;
+        // dense-output coefficients (FourthOrderPolynomialInterpolation)
+        float acc = kM[0] * k0;
+        acc = __builtin_fmaf(kM[2], k2, acc);
+        acc = __builtin_fmaf(kM[3], k3, acc);
+        acc = __builtin_fmaf(kM[4], k4, acc);
+        acc = __builtin_fmaf(kM[5], k5, acc);
+        acc = __builtin_fmaf(kM[6], k6, acc);
+        const float ym = yy0 + acc;
+        ca[m] = ((2.0f * (k6 - k0)) - (8.0f * (yy1 + yy0))) + (16.0f * ym);
+        cb[m] = ((((5.0f * k0) - (3.0f * k6)) + (18.0f * yy0)) + (14.0f * yy1)) - (32.0f * ym);
+        cc[m] = (((k6 - (4.0f * k0)) - (11.0f * yy0)) - (5.0f * yy1)) + (16.0f * ym);
+        k0v[m] = k0;
+        y0v[m] = yy0;
     }
     const float mean = wave_sum_f32(part) / (float)N;
     const float err = sqrtf(mean);
@@ -319,26 +399,7 @@ __device__ __forceinline__ void post_step(const DevParams& p, Ctl& c, int env, f
     fac = fac < 10.0f ? fac : 10.0f;
     const float dtn = h * fac;
     if (keep) {
-        float ca[EPL], cb[EPL], cc[EPL], k0v[EPL], y0v[EPL], y1v[EPL];
-#pragma unroll
-        for (int m = 0; m < EPL; ++m) {
-            const int i = lane + 64 * m;
-            const float k0 = h * Fe[i], k6 = h * Fe[6 * N + i];
-            float acc = kM1 * k0;
-            acc = __builtin_fmaf(kM3, h * Fe[2 * N + i], acc);
-            acc = __builtin_fmaf(kM4, h * Fe[3 * N + i], acc);
-            acc = __builtin_fmaf(kM5, h * Fe[4 * N + i], acc);
-            acc = __builtin_fmaf(kM6, h * Fe[5 * N + i], acc);
-            acc = __builtin_fmaf(kM7, k6, acc);
-            const float yy0 = y0p[i], yy1 = y1p[i];
-            const float ym = yy0 + acc;
-            ca[m] = ((2.0f * (k6 - k0)) - (8.0f * (yy1 + yy0))) + (16.0f * ym);
-            cb[m] = ((((5.0f * k0) - (3.0f * k6)) + (18.0f * yy0)) + (14.0f * yy1)) - (32.0f * ym);
-            cc[m] = (((k6 - (4.0f * k0)) - (11.0f * yy0)) - (5.0f * yy1)) + (16.0f * ym);
-            k0v[m] = k0;
-            y0v[m] = yy0;
-            y1v[m] = yy1;
-        }
+#pragma unroll 1
         while (c.si < c.g.n) {
             const float ts = (float)grid_at(c.g, c.si);
             if (!(ts <= c.tnext)) break;
@@ -358,11 +419,11 @@ __device__ __forceinline__ void post_step(const DevParams& p, Ctl& c, int env, f
                 lfp_of_row<EPL>(p, env, row, &ln, &lr);
                 const int pos = c.si - c.lfp_from + c.pos0;
                 if (lane == 0) {
-                    if (ring_dst) {
-                        ring_dst[pos] = lr;
+                    if (to_ring) {
+                        p.ring[(size_t)env * p.W + pos] = lr;
                     } else {
-                        smp_n[pos] = ln;
-                        smp_r[pos] = lr;
+                        s_smp_n[e][pos] = ln;
+                        s_smp_r[e][pos] = lr;
                     }
                 }
             }
@@ -372,11 +433,12 @@ __device__ __forceinline__ void post_step(const DevParams& p, Ctl& c, int env, f
             }
             c.si++;
         }
+        // y0 <- y1, f0 <- f6 (FSAL)
+        float2* rec2 = reinterpret_cast<float2*>(p.R + (size_t)env * N * 8) + 4 * lane;
 #pragma unroll
         for (int m = 0; m < EPL; ++m) {
-            const int i = lane + 64 * m;
-            y0p[i] = y1v[m];
-            Fe[i] = Fe[6 * N + i];
+            const float f6 = p.R[((size_t)env * N + lane + 64 * m) * 8 + 7];
+            rec2[4 * 64 * m] = make_float2(y1p[64 * m], f6);
         }
         c.tprev = c.tnext;
     } else {
@@ -397,61 +459,73 @@ __device__ __forceinline__ void post_step(const DevParams& p, Ctl& c, int env, f
 // One diffeqsolve for the workgroup's envs (each wave drives its 2 envs'
 // control; the coupling GEMM always covers all 16 rows).
 template <int TPW>
-__device__ void solve_wg(const DevParams& p, float* Xs, int* wg_flag, Ctl (&ctl)[ENVS_PER_WAVE], int env_base,
-                         float (*smp_n)[KURA_S_MAX + 2], double (*smp_r)[KURA_S_MAX + 2], bool to_ring,
-                         long long* rhs_count) {
+__device__ void solve_wg(const DevParams& p, float* Xs, Ctl (&ctl)[ENVS_PER_WAVE], int env_base, bool to_ring,
+                         bool pulse_on, long long* rhs_count) {
     constexpr int EPL = TPW * 4;  // N / 64
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int N = p.N;
-    floatx16 acc[TPW];
-    // Y0 <- state y for active envs; initial RHS (stage 0)
-#pragma unroll
+    constexpr int N = TPW * 256;
+    // record.y0 <- state y for active envs
+#pragma unroll 1
     for (int ee = 0; ee < ENVS_PER_WAVE; ++ee) {
         const int env = env_base + wave * ENVS_PER_WAVE + ee;
         if (env >= p.B || !ctl[ee].active) continue;
-#pragma unroll 4
+#pragma unroll
         for (int m = 0; m < EPL; ++m) {
             const size_t o = (size_t)env * N + lane + 64 * m;
-            p.Y0[o] = p.y[o];
+            p.R[o * 8] = p.y[o];
         }
     }
-    __syncthreads();
-    stage_input<EPL>(p, Xs, ctl, env_base, 0);
-    __syncthreads();
-    coupling_gemm<TPW>(Xs, p.alpha_sw, N, acc);
-    coupling_epilogue<TPW>(p, Xs, acc, env_base, 0);
-    long long nrhs = 1;
+    __syncthreads();  // pulse / records written above are visible to every lane
+    STAMP_DECL
+    long long nrhs = 0;
+    int s = 0;  // stage 0 = initial RHS at y0 (FSAL seed)
     for (;;) {
-        // workgroup-wide "any env still integrating?"
+        floatx16 acc[TPW];
+        EpiConst<TPW> kc;
+        stage_input<EPL>(p, Xs, ctl, env_base, s);
+        STAMP(0);
+        load_epi_const<TPW>(p, env_base, pulse_on, kc);
         __syncthreads();
-        if (threadIdx.x == 0) *wg_flag = 0;
+        STAMP(1);
+        coupling_gemm<TPW>(Xs, p.alpha_sw, acc);
+        STAMP(2);
+        coupling_epilogue<TPW>(p, Xs, acc, kc, env_base, s);
+        STAMP(3);
+        __syncthreads();
+        STAMP(4);
+        ++nrhs;
+        if (s > 0 && s < 6) {
+            ++s;
+            continue;
+        }
+        if (s == 6) {
+#pragma unroll 1
+            for (int ee = 0; ee < ENVS_PER_WAVE; ++ee) {
+                const int e = wave * ENVS_PER_WAVE + ee;
+                const int env = env_base + e;
+                if (env >= p.B || !ctl[ee].active) continue;
+                post_step<EPL>(p, ctl[ee], env, e, to_ring);
+            }
+            STAMP(5);
+        }
+        // workgroup-wide "any env still integrating?"
+        if (threadIdx.x == 0) s_wg_flag = 0;
         __syncthreads();
         int mine = 0;
 #pragma unroll
         for (int ee = 0; ee < ENVS_PER_WAVE; ++ee) mine |= ctl[ee].active;
-        if (mine && lane == 0) atomicOr(wg_flag, 1);
+        if (mine && lane == 0) atomicOr(&s_wg_flag, 1);
         __syncthreads();
-        if (*wg_flag == 0) break;
+        const int any = s_wg_flag;
+        __syncthreads();
+        STAMP(6);
+        if (any == 0) break;
 #pragma unroll
         for (int ee = 0; ee < ENVS_PER_WAVE; ++ee)
             if (ctl[ee].active) ctl[ee].h = ctl[ee].tnext - ctl[ee].tprev;
-        for (int s = 1; s <= 6; ++s) {
-            stage_input<EPL>(p, Xs, ctl, env_base, s);
-            __syncthreads();
-            coupling_gemm<TPW>(Xs, p.alpha_sw, N, acc);
-            coupling_epilogue<TPW>(p, Xs, acc, env_base, s);
-            __syncthreads();
-        }
-        nrhs += 6;
-#pragma unroll
-        for (int ee = 0; ee < ENVS_PER_WAVE; ++ee) {
-            const int e = wave * ENVS_PER_WAVE + ee;
-            const int env = env_base + e;
-            if (env >= p.B || !ctl[ee].active) continue;
-            double* rd = to_ring ? p.ring + (size_t)env * p.W : nullptr;
-            post_step<EPL>(p, ctl[ee], env, smp_n[e], smp_r[e], rd);
-        }
+        s = 1;
     }
+    STAMP_FLUSH(p);
     *rhs_count += nrhs;
 }
 
@@ -524,7 +598,7 @@ __device__ double serial_r64_f64(const double* v, int n) {
 // untouched slot of the ring or one of the S new samples held in LDS.
 struct WinView {
     const double* ring;
-    const double* fresh;
+    int e;
     int W, wp0, S;
     __device__ double at(int i) const {
         const int keep = W - S;
@@ -533,7 +607,7 @@ struct WinView {
             if (k >= W) k -= W;
             return ring[k];
         }
-        return fresh[i - keep];
+        return s_smp_r[e][i - keep];
     }
 };
 
@@ -606,10 +680,7 @@ __global__ __launch_bounds__(NTHREADS) void kura_step_kernel(DevParams p, const 
                                                              float* __restrict__ obs, double* __restrict__ reward,
                                                              uint8_t* __restrict__ done, float* __restrict__ lfp_true,
                                                              double* __restrict__ lfp_rec, int* __restrict__ nsamp) {
-    extern __shared__ float Xs[];  // 32 * N floats
-    __shared__ float smp_n[E_WG][KURA_S_MAX + 2];
-    __shared__ double smp_r[E_WG][KURA_S_MAX + 2];
-    __shared__ int wg_flag;
+    extern __shared__ float Xs[];  // xs_floats(N)
     constexpr int EPL = TPW * 4;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int N = p.N;
@@ -652,7 +723,8 @@ __global__ __launch_bounds__(NTHREADS) void kura_step_kernel(DevParams p, const 
         }
     }
     long long rhs = 0;
-    solve_wg<TPW>(p, Xs, &wg_flag, ctl, env_base, smp_n, smp_r, false, &rhs);
+    __syncthreads();
+    solve_wg<TPW>(p, Xs, ctl, env_base, false, true, &rhs);
     // ---- stimulation OFF (env.py:433-441)
 #pragma unroll
     for (int ee = 0; ee < ENVS_PER_WAVE; ++ee) {
@@ -675,11 +747,11 @@ __global__ __launch_bounds__(NTHREADS) void kura_step_kernel(DevParams p, const 
             flg[ee] |= 8;
         }
         if (lane == 0) {  // ys_II[0] == ys_I[-1]: duplicated sample (env.py:440)
-            smp_n[e][nI[ee]] = smp_n[e][nI[ee] - 1];
-            smp_r[e][nI[ee]] = smp_r[e][nI[ee] - 1];
+            s_smp_n[e][nI[ee]] = s_smp_n[e][nI[ee] - 1];
+            s_smp_r[e][nI[ee]] = s_smp_r[e][nI[ee] - 1];
         }
     }
-    solve_wg<TPW>(p, Xs, &wg_flag, ctl, env_base, smp_n, smp_r, false, &rhs);
+    solve_wg<TPW>(p, Xs, ctl, env_base, false, false, &rhs);
     __syncthreads();
     // ---- window, reward, outputs (env.py:443-454)
     constexpr int WPL = WPL_MAX;
@@ -706,7 +778,7 @@ __global__ __launch_bounds__(NTHREADS) void kura_step_kernel(DevParams p, const 
         const int W = p.W;
         double* rb = p.ring + (size_t)env * W;
         const int wp0 = p.wpos[env];
-        const WinView xv{rb, &smp_r[e][0], W, wp0, S};
+        const WinView xv{rb, e, W, wp0, S};
         double x[WPL];
 #pragma unroll
         for (int m = 0; m < WPL; ++m) {
@@ -724,7 +796,7 @@ __global__ __launch_bounds__(NTHREADS) void kura_step_kernel(DevParams p, const 
         if (lane < S) {
             int k = wp0 + lane;
             if (k >= W) k -= W;
-            rb[k] = smp_r[e][lane];
+            rb[k] = s_smp_r[e][lane];
         }
         int wp = wp0 + S;
         if (wp >= W) wp -= W;
@@ -738,8 +810,8 @@ __global__ __launch_bounds__(NTHREADS) void kura_step_kernel(DevParams p, const 
             if (nsamp) nsamp[env] = S;
         }
         if (lane < KURA_S_MAX) {
-            if (lfp_true) lfp_true[(size_t)env * KURA_S_MAX + lane] = lane < S ? smp_n[e][lane] : 0.0f;
-            if (lfp_rec) lfp_rec[(size_t)env * KURA_S_MAX + lane] = lane < S ? smp_r[e][lane] : 0.0;
+            if (lfp_true) lfp_true[(size_t)env * KURA_S_MAX + lane] = lane < S ? s_smp_n[e][lane] : 0.0f;
+            if (lfp_rec) lfp_rec[(size_t)env * KURA_S_MAX + lane] = lane < S ? s_smp_r[e][lane] : 0.0;
         }
     }
     flush_stats(p, rhs, ctl, env_base);
@@ -751,12 +823,10 @@ __global__ __launch_bounds__(NTHREADS) void kura_reset_kernel(DevParams p, const
                                                               const float* __restrict__ theta0,
                                                               float* __restrict__ obs) {
     extern __shared__ float Xs[];
-    __shared__ float smp_n[E_WG][KURA_S_MAX + 2];
-    __shared__ double smp_r[E_WG][KURA_S_MAX + 2];
-    __shared__ int wg_flag;
     constexpr int EPL = TPW * 4;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int N = p.N, W = p.W;
+    const int N = p.N;
+    const int W = p.W;
     const int env_base = blockIdx.x * E_WG;
     Ctl ctl[ENVS_PER_WAVE];
 #pragma unroll
@@ -776,7 +846,7 @@ __global__ __launch_bounds__(NTHREADS) void kura_reset_kernel(DevParams p, const
         ctl_begin(ctl[ee], g, p.dt0, g.n - 1 - W, g.n - 1, 0);
     }
     long long rhs = 0;
-    solve_wg<TPW>(p, Xs, &wg_flag, ctl, env_base, smp_n, smp_r, true, &rhs);
+    solve_wg<TPW>(p, Xs, ctl, env_base, true, false, &rhs);
     __syncthreads();
 #pragma unroll
     for (int ee = 0; ee < ENVS_PER_WAVE; ++ee) {
@@ -810,7 +880,7 @@ __global__ __launch_bounds__(64) void kura_reward_kernel(DevParams p, const doub
     }
     double* ext = p.scratch + (size_t)p.B * 2 * (p.W + 2 * p.padlen) + (size_t)env * 2 * (p.W + 2 * p.padlen);
     double* tmp = ext + (p.W + 2 * p.padlen);
-    const WinView xv{xl, xl, p.W, 0, 0};
+    const WinView xv{xl, 0, p.W, 0, 0};
     const double r = reward_of<WPL>(p, x, (double)u0[env], xv, ext, tmp);
     if (lane == 0) out[env] = r;
 }
@@ -842,7 +912,7 @@ __global__ __launch_bounds__(NTHREADS) void kura_selftest_gemm_kernel(const floa
     }
     __syncthreads();
     floatx16 acc[TPW];
-    coupling_gemm<TPW>(Xs, alpha_sw, N, acc);
+    coupling_gemm<TPW>(Xs, alpha_sw, acc);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
     for (int t = 0; t < TPW; ++t)

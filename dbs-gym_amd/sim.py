@@ -72,11 +72,11 @@ def make_config(params: dict, n_envs: int, reward_func: str | None = None, max_s
 class KuraSim:
     """B environments on one GPU behind libkura."""
 
-    def __init__(self, cfg: KuraConfig, device: torch.device | str | int = 0):
+    def __init__(self, cfg: KuraConfig, device: torch.device | str | int = 0, lib_path: str | None = None):
         if not torch.cuda.is_available():
             raise RuntimeError("KuraSim needs a ROCm GPU (torch.cuda.is_available() is False); "
                                "there is no CPU implementation of the step path")
-        self.lib = abi.load_library()
+        self.lib = abi.load_library(lib_path)
         self.cfg = cfg
         self.device = torch.device("cuda", torch.device(device).index if not isinstance(device, int) else device)
         if self.device.index is None:
@@ -171,6 +171,11 @@ class KuraSim:
     def stats(self) -> np.ndarray:
         out = np.zeros(4, np.int64)
         check(self.lib, self.lib.kura_get_stats(self._h, out.ctypes.data), "kura_get_stats")
+        return out
+
+    def stamps(self) -> np.ndarray:
+        out = np.zeros((8, 8), np.uint64)
+        check(self.lib, self.lib.kura_get_stamps(self._h, out.ctypes.data), "kura_get_stamps")
         return out
 
     def close(self) -> None:

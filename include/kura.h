@@ -127,6 +127,10 @@ int kura_get_stats(KuraHandle* h, int64_t* out4);
  * 32 x N operand: Y[r][i] = sum_k X[r][k] * alpha[i][k]. */
 int kura_selftest_math(const float* x, const float* y, float* out, int n);
 int kura_selftest_gemm(const float* X, const float* alpha, float* Y, int N);
+/* per-wave phase cycle counters of a -DKURA_STAMPS build ([8 waves][8]:
+ * stage-input, barrier, GEMM, epilogue, barrier, post-step, flag, start);
+ * zeros in the production build.  Reading clears them. */
+int kura_get_stamps(KuraHandle* h, uint64_t* out);
 
 #ifdef __cplusplus
 }

@@ -37,7 +37,7 @@ def lib() -> ctypes.CDLL:
         L.oracle_reset.restype = c_int
         L.oracle_reset.argtypes = [c_void_p, c_int] + [c_void_p] * 10
         L.oracle_step.restype = c_int
-        L.oracle_step.argtypes = [c_void_p, c_int] + [c_void_p] * 17
+        L.oracle_step.argtypes = [c_void_p, c_int] + [c_void_p] * 18
         L.oracle_solve_rows.restype = c_int
         L.oracle_solve_rows.argtypes = [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p]
         L.oracle_rhs.argtypes = [c_void_p] * 5

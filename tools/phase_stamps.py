@@ -1,0 +1,63 @@
+#!/usr/bin/env python3
+"""Diagnostic: per-phase cycle breakdown of kura_step_kernel (KURA_STAMPS build).
+
+Builds dbs-gym_amd/csrc/libkura_stamps.so with -DKURA_STAMPS and runs a few
+bench-shaped steps, printing the share of wave cycles in each phase."""
+import importlib
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import __graft_entry__ as ge  # noqa: E402
+
+LIB = os.path.join(ge.CSRC, "libkura_stamps.so")
+PHASES = ["stage_input", "barrier1", "gemm", "epilogue", "barrier2", "post_step", "flag_sync", "start"]
+
+
+def main():
+    if not os.path.exists(LIB) or os.path.getmtime(LIB) < os.path.getmtime(os.path.join(ge.CSRC, "kura_kernels.hip")):
+        subprocess.run([ge.HIPCC, *ge.HIP_FLAGS, "-DKURA_STAMPS", "-o", LIB,
+                        os.path.join(ge.CSRC, "kura_kernels.hip")], check=True)
+    import numpy as np
+    import torch
+    import bench
+    sim_mod = importlib.import_module("dbs-gym_amd.sim")
+
+    class A:
+        config = os.environ.get("CFG", "env0")
+        osc = int(os.environ.get("OSC", "1024"))
+        envs = int(os.environ.get("ENVS", "4096"))
+        reward = "bbpow_action"
+        seed = 7
+    cfg, alpha, omega, gs, gr, th0, ct, st = bench.build_shard(A, 0)
+    sim = sim_mod.KuraSim(cfg, 0, lib_path=LIB)
+    sim.set_coupling(alpha)
+    sim.set_env_params(omega, gs, gr)
+    sim.set_spectral(ct, st)
+    sim.reset(torch.from_numpy(th0))
+    torch.cuda.synchronize()
+    sim.stamps()
+    a = torch.zeros((cfg.n_envs, cfg.n_elec), device="cuda")
+    nsteps = 5
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0.record()
+    for _ in range(nsteps):
+        sim.step(a)
+    ev1.record()
+    torch.cuda.synchronize()
+    s = sim.stamps().astype(np.float64)
+    tot = s.sum(axis=1, keepdims=True)
+    share = (s / np.maximum(tot, 1)).mean(axis=0)
+    nwg = (cfg.n_envs + 15) // 16
+    cyc_per_step_wave = s.sum(axis=0) / (8 * nwg * nsteps)
+    out = {"ms_per_step": ev0.elapsed_time(ev1) / nsteps,
+           "share": dict(zip(PHASES, [round(float(x), 4) for x in share])),
+           "cycles_per_step_per_wave": dict(zip(PHASES, [round(float(x)) for x in cyc_per_step_wave]))}
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
