@@ -671,3 +671,12 @@ void oracle_gemm_chain(const float* X, const float* A, float* Y, int M, int N, i
             Y[(size_t)r * N + i] = acc;
         }
 }
+
+/* LFP of one row (naive fp32 mean of cos, and records) for golden tests. */
+void oracle_lfp(void* ctx, const float* row, const double* g_rec, float* naive, double* rec) {
+    OCtx* o = (OCtx*)ctx;
+    Work w;
+    if (work_alloc(&w, o->N)) return;
+    lfp_row(o, &w, row, g_rec, naive, rec);
+    work_free(&w);
+}

@@ -54,6 +54,7 @@ def lib() -> ctypes.CDLL:
         for n in ("oracle_fmod2pi", "oracle_inv_fifth_root"):
             getattr(L, n).argtypes = [c_void_p, c_void_p, c_int]
         L.oracle_gemm_chain.argtypes = [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int]
+        L.oracle_lfp.argtypes = [c_void_p] * 5
         _lib = L
     return _lib
 
@@ -130,6 +131,16 @@ class Oracle:
         lib().oracle_rhs(self._ctx, _p(np.ascontiguousarray(y, np.float32)), _p(np.ascontiguousarray(omega, np.float32)),
                          _p(np.ascontiguousarray(pulse, np.float32)), _p(f))
         return f
+
+    def lfp(self, row, g_rec=None):
+        """(naive fp32 LFP, records) of one saved row (env.py:396-412)."""
+        n = ctypes.c_float()
+        r = ctypes.c_double()
+        gr = (np.zeros((max(self.cfg.n_rec, 1), self.N)) if g_rec is None
+              else np.ascontiguousarray(g_rec, np.float64))
+        lib().oracle_lfp(self._ctx, _p(np.ascontiguousarray(row, np.float32)), _p(gr), ctypes.byref(n),
+                         ctypes.byref(r))
+        return n.value, r.value
 
     def reward(self, window, u0):
         return lib().oracle_reward(ctypes.byref(self.cfg), _p(np.ascontiguousarray(window, np.float64)), float(u0),

@@ -1,0 +1,81 @@
+"""Host-side logic: config derivation, validation errors, drift/spatial events."""
+import importlib
+
+import numpy as np
+import pytest
+
+from helpers import kura
+
+sim_mod = importlib.import_module("dbs-gym_amd.sim")
+ms = importlib.import_module("dbs-gym_amd.model_setup")
+
+
+def test_config_derivation_env0():
+    p = kura.reference_params("env0")
+    c = sim_mod.make_config(p, 7, reward_func="bbpow_action")
+    assert c.window == 2340                                  # env.py:297
+    assert c.episode_steps == 5555                           # env.py:300 (5000 units)
+    assert [c.bins[i] for i in range(c.n_bins)] == list(range(15, 25))  # 12.82..20.51 Hz
+    assert c.kn == np.float32(0.52 / 512)
+    assert c.padlen == 15 and c.n_elec == 1 and c.n_rec == 1
+    ce = sim_mod.make_config(kura.reference_params("env0", "eval", 0), 1, reward_func="bbpow_action")
+    assert ce.episode_steps == 1111
+
+
+def test_butterworth_matches_survey_constants():
+    b, a, zi = kura.spectral.butter_bandpass(0.05)
+    np.testing.assert_allclose(b, [7.6851e-4, 0, -1.5370e-3, 0, 7.6851e-4], atol=1e-7)
+    np.testing.assert_allclose(a, [1, -3.913104, 5.749636, -3.759662, 0.923142], atol=1e-6)
+
+
+@pytest.mark.parametrize("mut,exc", [
+    (lambda p: p.update(reward_func="nope"), ValueError),
+    (lambda p: p.update(recording_kernel="sharp"), ValueError),
+    (lambda p: p.update(transient_state_len=50.0), ValueError),
+    (lambda p: p.update(electrode_amps=[0.0, 1.0]), AssertionError),
+])
+def test_config_errors_mirror_reference(mut, exc):
+    p = kura.reference_params("env0")
+    p["reward_func"] = "bbpow_action"
+    mut(p)
+    with pytest.raises(exc):
+        sim_mod.make_config(p, 1)
+
+
+def _host(name, seed=0, split="train"):
+    p = kura.reference_params(name, split)
+    return kura.EnvHost(kura.fill_driver_arrays(p, w0_seed=seed))
+
+
+def test_env1_spatial_variation_schedule():
+    h = _host("env1")
+    coords = []
+    for _ in range(25):
+        h.reset_draws()
+        coords.append(list(map(list, h.elec_coords)))
+    assert all(c == [[4, 3, 4]] for c in coords[:10])
+    assert [ev[0] for ev in h.spatial_events] == [10, 20]
+    assert coords[10] in [[t[0]] for t in kura.configs.STIM_REC_LOCUS]
+
+
+def test_env2_drift_events_stay_on_grid():
+    h = _host("env2", seed=3)
+    enc = []
+    for _ in range(40):
+        w0, gs, gr, th = h.reset_draws()
+        assert np.all(w0 > 0) and np.all(np.isfinite(gs))
+        enc.append(h.encapsulation_coeff)
+        for c in h.elec_coords[0]:
+            assert 1 <= c <= 6
+    assert h.temporal_events["electrode_drift"] and h.temporal_events["plasticity_drift"]
+    assert enc[-1] > enc[0]  # raw accumulation
+
+
+def test_synthetic_grids():
+    for n, g in ((256, [8, 8, 4]), (512, [8, 8, 8]), (1024, [16, 8, 8])):
+        p = kura.synthetic_params("env0", n)
+        assert p["grid_size"] == g
+        coords, grid = ms.neuron_grid_3d(*g, n, 0.1)
+        assert coords.shape == (n, 3)
+        assert ms.flat_index(p["elec_coords"][0], g) < n
+        assert ms.flat_index(p["locus_center"], g) < n
