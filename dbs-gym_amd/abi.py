@@ -87,7 +87,7 @@ _SYMBOLS = {
     "kura_reset": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "kura_step": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                           c_void_p]),
-    "kura_reward": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p]),
+    "kura_reward": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p]),
     "kura_get_state": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "kura_set_state": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "kura_get_stats": (c_int, [c_void_p, c_void_p]),

@@ -142,13 +142,13 @@ class KuraSim:
         self._keep = (a,)
         return self.obs, self.reward, self.done
 
-    def reward_of(self, window: torch.Tensor, u0: torch.Tensor) -> torch.Tensor:
+    def reward_of(self, window: torch.Tensor, u0: torch.Tensor, kind: int = 0) -> torch.Tensor:
         w = window.to(self.device, torch.float64).contiguous()
         u = u0.to(self.device, torch.float32).contiguous()
         n = w.shape[0]
         out = torch.empty(n, dtype=torch.float64, device=self.device)
         with torch.cuda.device(self.device):
-            check(self.lib, self.lib.kura_reward(self._h, ptr(w), ptr(u), ptr(out), n, self._stream()),
+            check(self.lib, self.lib.kura_reward(self._h, int(kind), ptr(w), ptr(u), ptr(out), n, self._stream()),
                   "kura_reward")
         return out
 

@@ -108,7 +108,11 @@ int kura_step(KuraHandle* h, const float* action /* B*n_elec in [-1,1] */,
               double* lfp_rec,  /* B*KURA_S_MAX  theta_records, env.py:445 (may be NULL) */
               int32_t* nsamp,   /* B     samples emitted this step (17..19) */
               void* stream);
-int kura_reward(KuraHandle* h, const double* window /* n*W device */, const float* u0 /* n device */,
+/* reward of n given windows (oldest first) with first amplitudes u0 (already
+ * rescaled, env.py:419); kind = KURA_R_* or 0 for the handle's reward_kind.
+ * The reference exposes all three reward methods on every env (called
+ * directly by aDBS_RL/agents/simple_dbs.py:83-90). */
+int kura_reward(KuraHandle* h, int kind, const double* window /* n*W device */, const float* u0 /* n device */,
                 double* reward /* n device */, int n, void* stream);
 
 /* state snapshot for checkpoint/resume and parity tests (host pointers; syncs) */
