@@ -153,8 +153,14 @@ KDM_FN float kdm_inv_fifth_root(float xf) {
 }
 
 // ---- canonical reductions ---------------------------------------------
-// R64: the order in which every per-env sum over oscillators is taken.
-// lane l (0..63) accumulates x[l], x[l+64], x[l+128], ... in ascending order
-// (starting from +0), then lanes combine by an xor butterfly with offsets
-// 32,16,8,4,2,1 (p[l] = p[l] + p[l^o]).  This is exactly what one wavefront
-// does with a strided loop + __shfl_xor; the oracle replays it sequentially.
+// Two summation orders are part of the numerics contract (the oracle replays
+// both sequentially, oracle/kura_oracle.c):
+// RM  (sums over the N oscillators inside the solver: error norm, LFP) --
+//     the MFMA accumulator layout of the kernel: wave w (0..7) owns columns
+//     32*(w*TPW + t) + c, TPW = N/256; each column lane c sums its TPW values
+//     in t order from +0, the 32 lanes combine by an xor butterfly
+//     (16,8,4,2,1: p[c] = p[c] + p[c^o]), then the 8 wave totals are added in
+//     wave order from +0.
+// R64 (sums over the W-sample window: DFT bins, filtfilt mean) -- lane l
+//     (0..63) sums x[l], x[l+64], ... from +0, then an xor butterfly with
+//     offsets 32,16,8,4,2,1.

@@ -82,8 +82,7 @@ struct DevParams {
     int* step;              // [B]
     double* ring;           // [B][W] observation window ring
     int* wpos;              // [B] next write slot == oldest sample
-    float* R;               // [B][N][8] per-oscillator record {y0, f_0 .. f_6} (f_j = RHS at stage j)
-    float* Y1;              // [B][N]
+    float* R;               // [B/16][NSLOT][N][16] solver workspace: per slot, 16 envs per oscillator
     float* pulse;           // [B][N]
     double* scratch;        // [B][W + 2*padlen] * 2 (R2 filtfilt)
     unsigned long long* stats;  // [4]: max rhs, steps, rejected, flags
@@ -104,10 +103,9 @@ struct DevParams {
 #endif
 
 // Per-workgroup LDS besides the dynamic 32 x N operand: LFP samples of the
-// current step (one row per env) and the "any env still integrating" flag.
+// current step (one row per env).
 __shared__ float s_smp_n[E_WG][KURA_S_MAX + 2];
 __shared__ double s_smp_r[E_WG][KURA_S_MAX + 2];
-__shared__ int s_wg_flag;
 
 // LDS index of X[row][k] in MFMA A-fragment order: for k-block kb = k/8,
 // lane (row + 32*(k&1)) holds its 4 consecutive k-steps in 16 contiguous
@@ -148,14 +146,6 @@ __device__ __forceinline__ Grid make_grid(double start, double stop, double step
 __device__ __forceinline__ double grid_at(const Grid& g, int i) {
     return i == 0 ? g.start : g.start + (double)i * g.delta;
 }
-
-// Per-env solver control (wave-uniform; lives in the owning wave).
-struct Ctl {
-    Grid g;
-    float t1, tprev, tnext, h;
-    int si, active, nsteps, rejected, flags;
-    int lfp_from, lfp_to, pos0;  // which saved rows feed LFP samples, and where
-};
 
 // ---------------------------------------------------------------- GEMM ----
 // acc[t] (32 x 32 tile, columns jt = wave*TPW + t) = X (LDS) x B-fragments.
@@ -208,13 +198,88 @@ __device__ __forceinline__ void coupling_gemm(const float* __restrict__ Xs, cons
     }
 }
 
-// MFMA-layout element ownership: lane holds, for each of its TPW column tiles,
-// accumulator rows q = 0..7 (sin rows of env e(q)) and q+8 (cos rows of the
-// same env).  e(q) = (q&3) + 8(q>>2) + 4(lane>>5); column i = 32*jt + (lane&31).
+// Per-env solver control.  One slot per local env lives in LDS; thread e
+// (e < 16) owns slot e's scalar decisions, every lane reads it.
+struct CtlE {
+    double g_start, g_delta;  // save grid (np.arange start, (start+step)-start)
+    int n;                    // grid length
+    int si;                   // next save index
+    int active;               // still integrating in this solve
+    int nsteps, rejected, flags;
+    int lfp_from, lfp_to, pos0;  // rows [from,to) feed LFP samples at pos0 + (si - from)
+    int keep, nsave;          // decision of the last attempted step
+    int acc_steps, acc_rej;   // over the solves of one launch (stats)
+    float t1, tprev, tnext, h, dtn;
+};
+__shared__ CtlE s_ctl[E_WG];
+__shared__ float s_red[NWAVES][E_WG];            // per-wave partial sums (f32)
+__shared__ double s_redd[NWAVES][E_WG][4];       // per-wave partial sums (f64, per recorder)
+__shared__ float s_theta[E_WG];                  // dense-output abscissa of this save round
+__shared__ int s_rflag[E_WG];                    // bit0: save row, bit1: LFP row, bit2: final row
+__shared__ double s_u[E_WG][4];                  // rescaled amplitudes (env.py:389-393)
+__shared__ int s_maxsave, s_any;
+
+__device__ __forceinline__ double grid_at_c(const CtlE& c, int i) {
+    return i == 0 ? c.g_start : c.g_start + (double)i * c.g_delta;
+}
+
+// thread e: start a diffeqsolve over the grid (oracle solve() prologue)
+__device__ __forceinline__ void ctl_begin(CtlE& c, const Grid& g, float dt0, int lfp_from, int lfp_to, int pos0) {
+    c.g_start = g.start;
+    c.g_delta = g.delta;
+    c.n = g.n;
+    const float t0 = (float)grid_at(g, 0);
+    c.t1 = (float)grid_at(g, g.n - 1);
+    c.tprev = t0;
+    c.tnext = fminf(t0 + dt0, c.t1);
+    c.h = 0.0f;
+    c.dtn = 0.0f;
+    c.si = 0;
+    c.lfp_from = lfp_from;
+    c.lfp_to = lfp_to;
+    c.pos0 = pos0;
+    c.keep = 0;
+    c.nsave = 0;
+    c.acc_steps += c.nsteps;  // carry the previous solve's counters
+    c.acc_rej += c.rejected;
+    c.nsteps = 0;
+    c.rejected = 0;
+    c.active = g.n >= 2;
+}
+
+// MFMA-layout element ownership: lane holds, for each of its TPW column tiles
+// t, accumulator rows q = 0..7 (sin rows) and q+8 (cos rows) of local env
+// e(q) = (q&3) + 8(q>>2) + 4(lane>>5) at column i = 32(wave*TPW + t) + (lane&31).
+// Workspace records are [slot][i][16 envs] per workgroup, so q = 0..3 and
+// q = 4..7 are two 16-byte vectors at envs 4h.. and 8+4h...
 __device__ __forceinline__ int mfma_env(int q, int lane) { return (q & 3) + 8 * (q >> 2) + 4 * (lane >> 5); }
 
+enum { SL_Y0 = 0, SL_F0 = 1, SL_Y1 = 8, SL_CA = 9, SL_CB = 10, SL_CC = 11, NSLOT = 12 };
+
+struct Slot {
+    float* base;  // workgroup slot 0
+    int N;
+    __device__ floatx4* at(int slot, int i, int half) const {
+        return reinterpret_cast<floatx4*>(base + ((size_t)slot * N + i) * 16) + half;
+    }
+};
+
+__device__ __forceinline__ void split8(const floatx4& a, const floatx4& b, float (&v)[8]) {
+    v[0] = a[0]; v[1] = a[1]; v[2] = a[2]; v[3] = a[3];
+    v[4] = b[0]; v[5] = b[1]; v[6] = b[2]; v[7] = b[3];
+}
+// lane's two env groups: half 0 -> envs 4h..4h+3, half 1 -> envs 8+4h..8+4h+3
+__device__ __forceinline__ void load8(const Slot& w, int slot, int i, int hq, float (&v)[8]) {
+    split8(*w.at(slot, i, hq), *w.at(slot, i, 2 + hq), v);
+}
+__device__ __forceinline__ void store8(const Slot& w, int slot, int i, int hq, const float (&v)[8]) {
+    floatx4 a = {v[0], v[1], v[2], v[3]}, b = {v[4], v[5], v[6], v[7]};
+    *w.at(slot, i, hq) = a;
+    *w.at(slot, i, 2 + hq) = b;
+}
+
 // omega and pulse of the lane's MFMA-layout elements, fetched at the start of
-// the GEMM so their latency hides under the K loop.
+// a stage so their latency hides under the GEMM.
 template <int TPW>
 struct EpiConst {
     float w[TPW][8];
@@ -240,256 +305,368 @@ __device__ __forceinline__ void load_epi_const(const DevParams& p, int env_base,
     }
 }
 
-// f = fmaf(kn, fmaf(c, P, -(s*Q)), omega) + pulse  ->  R[env][i][1 + stage]
+// f = fmaf(kn, fmaf(c, P, -(s*Q)), omega) + pulse  ->  slot F0 + stage
 template <int TPW>
-__device__ __forceinline__ void coupling_epilogue(const DevParams& p, const float* __restrict__ Xs,
-                                                  const floatx16 (&acc)[TPW], const EpiConst<TPW>& kc,
-                                                  int env_base, int stage) {
+__device__ __forceinline__ void coupling_epilogue(const DevParams& p, const Slot& ws, const float* __restrict__ Xs,
+                                                  const floatx16 (&acc)[TPW], const EpiConst<TPW>& kc, int stage) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    constexpr int N = TPW * 256;
+    const int hq = lane >> 5;
 #pragma unroll
     for (int t = 0; t < TPW; ++t) {
         const int i = 32 * (wave * TPW + t) + (lane & 31);
+        float f[8];
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
             const int e = mfma_env(q, lane);
-            const int env = env_base + e;
             const float P = acc[t][q], Q = acc[t][q + 8];
             const float sn = Xs[xs_idx(e, i)], cs = Xs[xs_idx(16 + e, i)];
             const float tq = sn * Q;
             const float coup = __builtin_fmaf(cs, P, -tq);
-            const float f = __builtin_fmaf(p.kn, coup, kc.w[t][q]) + kc.u[t][q];
-            if (env < p.B) p.R[((size_t)env * N + i) * 8 + 1 + stage] = f;
+            f[q] = __builtin_fmaf(p.kn, coup, kc.w[t][q]) + kc.u[t][q];
         }
+        store8(ws, SL_F0 + stage, i, hq, f);
     }
 }
 
-// ------------------------------------------------------------ R64 stages ---
 // Stage input ys = y0 + chain_j(A[s][j] * h*f_j) (zero coefficients skipped,
-// as in the oracle), theta = fmod(ys, 2pi) and sin/cos into the LDS operand.
-// Stage 0 is the solve's initial RHS at y0.  Each element's record is read
-// with one or two 16-byte loads; 8 elements are in flight per batch.
-template <int EPL>
-__device__ __forceinline__ void stage_input(const DevParams& p, float* Xs, const Ctl (&ctl)[ENVS_PER_WAVE],
-                                            int env_base, int s) {
+// as in the oracle), theta = fmod(ys, 2pi), sin/cos into the LDS operand.
+// Stage 0 is the solve's initial RHS at y0.
+template <int TPW>
+__device__ __forceinline__ void stage_input(const Slot& ws, float* Xs, int s) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    constexpr int N = EPL * 64;
-    constexpr int CH = EPL < 8 ? EPL : 8;
-#pragma unroll 1
-    for (int ee = 0; ee < ENVS_PER_WAVE; ++ee) {
-        const int e = wave * ENVS_PER_WAVE + ee;
-        const int env = env_base + e;
-        if (env >= p.B || !ctl[ee].active) continue;
-        const float h = ctl[ee].h;
-        const floatx4* rec = reinterpret_cast<const floatx4*>(p.R + (size_t)env * N * 8) + 2 * lane;
-#pragma unroll 1
-        for (int m0 = 0; m0 < EPL; m0 += CH) {
-            floatx4 lo[CH], hi[CH];
+    const int hq = lane >> 5;
+    float h[8];
 #pragma unroll
-            for (int m = 0; m < CH; ++m) {
-                lo[m] = rec[2 * 64 * (m0 + m)];
-                if (s >= 4) hi[m] = rec[2 * 64 * (m0 + m) + 1];
-            }
+    for (int q = 0; q < 8; ++q) h[q] = s_ctl[mfma_env(q, lane)].h;
+#pragma unroll 1
+    for (int t = 0; t < TPW; ++t) {
+        const int i = 32 * (wave * TPW + t) + (lane & 31);
+        float y0[8], f[6][8];
+        load8(ws, SL_Y0, i, hq, y0);
 #pragma unroll
-            for (int m = 0; m < CH; ++m) {
-                const int i = lane + 64 * (m0 + m);
-                // record: lo = {y0, f0, f1, f2}, hi = {f3, f4, f5, f6}
-                float ys = lo[m][0];
-                if (s > 0) {
-                    float acc = cA[s][0] * (h * lo[m][1]);
-                    if (s > 1 && cA[s][1] != 0.0f) acc = __builtin_fmaf(cA[s][1], h * lo[m][2], acc);
-                    if (s > 2) acc = __builtin_fmaf(cA[s][2], h * lo[m][3], acc);
-                    if (s > 3) acc = __builtin_fmaf(cA[s][3], h * hi[m][0], acc);
-                    if (s > 4) acc = __builtin_fmaf(cA[s][4], h * hi[m][1], acc);
-                    if (s > 5) acc = __builtin_fmaf(cA[s][5], h * hi[m][2], acc);
-                    ys = lo[m][0] + acc;
-                    if (s == 6) p.Y1[(size_t)env * N + i] = ys;
-                }
-                float sn, cs;
-                kdm_sincosf(kdm_fmod2pi(ys), &sn, &cs);
-                Xs[xs_idx(e, i)] = sn;
-                Xs[xs_idx(16 + e, i)] = cs;
+        for (int j = 0; j < 6; ++j)
+            if (j < s) load8(ws, SL_F0 + j, i, hq, f[j]);
+        float ys[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            float v = y0[q];
+            if (s > 0) {
+                float acc = cA[s][0] * (h[q] * f[0][q]);
+                if (s > 1 && cA[s][1] != 0.0f) acc = __builtin_fmaf(cA[s][1], h[q] * f[1][q], acc);
+                if (s > 2) acc = __builtin_fmaf(cA[s][2], h[q] * f[2][q], acc);
+                if (s > 3) acc = __builtin_fmaf(cA[s][3], h[q] * f[3][q], acc);
+                if (s > 4) acc = __builtin_fmaf(cA[s][4], h[q] * f[4][q], acc);
+                if (s > 5) acc = __builtin_fmaf(cA[s][5], h[q] * f[5][q], acc);
+                v = y0[q] + acc;
             }
+            ys[q] = v;
+            float sn, cs;
+            kdm_sincosf(kdm_fmod2pi(v), &sn, &cs);
+            const int e = mfma_env(q, lane);
+            Xs[xs_idx(e, i)] = sn;
+            Xs[xs_idx(16 + e, i)] = cs;
         }
+        if (s == 6) store8(ws, SL_Y1, i, hq, ys);
     }
 }
 
-// LFP of one saved row (values in registers, R64 layout) -> (naive, records).
-template <int EPL>
-__device__ __forceinline__ void lfp_of_row(const DevParams& p, int env, const float (&row)[EPL], float* naive,
-                                           double* rec) {
-    const int lane = threadIdx.x & 63;
-    constexpr int N = EPL * 64;
-    float cr[EPL];
-    float part = 0.0f;
+// RM reduction (kura_detmath.h): per-lane partials (t order) -> 32-lane xor
+// butterfly -> s_red[wave][e]; the caller barriers, then thread e adds the
+// 8 wave totals in wave order.
+__device__ __forceinline__ void rm_publish(const float (&part)[8]) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
-    for (int m = 0; m < EPL; ++m) {
-        cr[m] = kdm_cosf(row[m]);
-        part = part + cr[m];
-    }
-    const float mean = wave_sum_f32(part) / (float)N;
-    *naive = mean;
-    if (p.rec_kernel == KURA_REC_GAUSSIAN) {
-        double acc = 0.0;
-        for (int r = 0; r < p.n_rec; ++r) {
-            const double* g = p.g_rec + ((size_t)env * p.n_rec + r) * N;
-            double pr = 0.0;
+    for (int q = 0; q < 8; ++q) {
+        float v = part[q];
 #pragma unroll
-            for (int m = 0; m < EPL; ++m) pr = pr + (double)cr[m] * g[lane + 64 * m];
-            acc = acc + wave_sum_f64(pr) / (double)N;
-        }
-        *rec = acc;
-    } else {
-        *rec = (double)mean;
+        for (int o = 16; o >= 1; o >>= 1) v = v + __shfl_xor(v, o, 64);
+        if ((lane & 31) == 0) s_red[wave][mfma_env(q, lane)] = v;
     }
 }
-
-// After the 7th stage: error norm, accept/reject, dense-output saves, FSAL.
-// One pass over the env's lane elements reads each record (two 16-byte loads)
-// and y1, forms the scaled error and the dense-output coefficients; then the
-// R64 reduction decides acceptance and the saves are evaluated from registers.
-template <int EPL>
-__device__ __forceinline__ void post_step(const DevParams& p, Ctl& c, int env, int e, bool to_ring) {
-    const int lane = threadIdx.x & 63;
-    constexpr int N = EPL * 64;
-    const float h = c.h;
-    floatx4* rec = reinterpret_cast<floatx4*>(p.R + (size_t)env * N * 8) + 2 * lane;
-    const float* y1p = p.Y1 + (size_t)env * N + lane;
-    float ca[EPL], cb[EPL], cc[EPL], k0v[EPL], y0v[EPL];
-    float part = 0.0f;
+__device__ __forceinline__ void rm_publish_d(const double (&part)[8], int r) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
-    for (int m = 0; m < EPL; ++m) {
-        const floatx4 lo = rec[2 * 64 * m], hi = rec[2 * 64 * m + 1];
-        const float yy1 = y1p[64 * m];
-        const float yy0 = lo[0];
-        const float k0 = h * lo[1], k2 = h * lo[3], k3 = h * hi[0], k4 = h * hi[1], k5 = h * hi[2],
-                    k6 = h * hi[3];
-        // error estimate (b_sol - b_embedded) and its scaled square
-        float er = kE[0] * k0;
-        er = __builtin_fmaf(kE[2], k2, er);
-        er = __builtin_fmaf(kE[3], k3, er);
-        er = __builtin_fmaf(kE[4], k4, er);
-        er = __builtin_fmaf(kE[5], k5, er);
-        er = __builtin_fmaf(kE[6], k6, er);
-        const float a0 = fabsf(yy0), a1 = fabsf(yy1);
-        const float mx = a0 > a1 ? a0 : a1;
-        const float den = p.atol + mx * p.rtol;
-        const float qe = er / den;
-        part = part + qe * qe;
-        // dense-output coefficients (FourthOrderPolynomialInterpolation)
-        float acc = kM[0] * k0;
-        acc = __builtin_fmaf(kM[2], k2, acc);
-        acc = __builtin_fmaf(kM[3], k3, acc);
-        acc = __builtin_fmaf(kM[4], k4, acc);
-        acc = __builtin_fmaf(kM[5], k5, acc);
-        acc = __builtin_fmaf(kM[6], k6, acc);
-        const float ym = yy0 + acc;
-        ca[m] = ((2.0f * (k6 - k0)) - (8.0f * (yy1 + yy0))) + (16.0f * ym);
-        cb[m] = ((((5.0f * k0) - (3.0f * k6)) + (18.0f * yy0)) + (14.0f * yy1)) - (32.0f * ym);
-        cc[m] = (((k6 - (4.0f * k0)) - (11.0f * yy0)) - (5.0f * yy1)) + (16.0f * ym);
-        k0v[m] = k0;
-        y0v[m] = yy0;
+    for (int q = 0; q < 8; ++q) {
+        double v = part[q];
+#pragma unroll
+        for (int o = 16; o >= 1; o >>= 1) v = v + __shfl_xor(v, o, 64);
+        if ((lane & 31) == 0) s_redd[wave][mfma_env(q, lane)][r] = v;
     }
-    const float mean = wave_sum_f32(part) / (float)N;
-    const float err = sqrtf(mean);
-    const bool keep = err < 1.0f;
-    float fac = 0.9f * kdm_inv_fifth_root(err);
-    const float fmn = keep ? 1.0f : 0.2f;
-    fac = fac > fmn ? fac : fmn;
-    fac = fac < 10.0f ? fac : 10.0f;
-    const float dtn = h * fac;
-    if (keep) {
-#pragma unroll 1
-        while (c.si < c.g.n) {
-            const float ts = (float)grid_at(c.g, c.si);
-            if (!(ts <= c.tnext)) break;
-            const float th = (ts - c.tprev) / (c.tnext - c.tprev);
-            float row[EPL];
+}
+__device__ __forceinline__ float rm_total(int e) {
+    float tot = 0.0f;
 #pragma unroll
-            for (int m = 0; m < EPL; ++m) {
-                float v = ca[m] * th + cb[m];
-                v = v * th + cc[m];
-                v = v * th + k0v[m];
-                v = v * th + y0v[m];
-                row[m] = v;
+    for (int w = 0; w < NWAVES; ++w) tot = tot + s_red[w][e];
+    return tot;
+}
+__device__ __forceinline__ double rm_total_d(int e, int r) {
+    double tot = 0.0;
+#pragma unroll
+    for (int w = 0; w < NWAVES; ++w) tot = tot + s_redd[w][e][r];
+    return tot;
+}
+
+// After the 7th stage: error norm, accept/reject, dense-output saves with
+// LFP, FSAL -- for all 16 envs, every wave on its own columns.
+template <int TPW>
+__device__ __forceinline__ void post_step(const DevParams& p, const Slot& ws, int env_base, bool to_ring) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, tid = threadIdx.x;
+    const int hq = lane >> 5;
+    constexpr int N = TPW * 256;
+    float h[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) h[q] = s_ctl[mfma_env(q, lane)].h;
+    // (1) scaled error partials and dense-output coefficients
+    float part[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll 1
+    for (int t = 0; t < TPW; ++t) {
+        const int i = 32 * (wave * TPW + t) + (lane & 31);
+        float y0[8], y1[8], f0[8], f2[8], f3[8], f4[8], f5[8], f6[8];
+        load8(ws, SL_Y0, i, hq, y0);
+        load8(ws, SL_Y1, i, hq, y1);
+        load8(ws, SL_F0 + 0, i, hq, f0);
+        load8(ws, SL_F0 + 2, i, hq, f2);
+        load8(ws, SL_F0 + 3, i, hq, f3);
+        load8(ws, SL_F0 + 4, i, hq, f4);
+        load8(ws, SL_F0 + 5, i, hq, f5);
+        load8(ws, SL_F0 + 6, i, hq, f6);
+        float ca[8], cb[8], cc[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const float k0 = h[q] * f0[q], k2 = h[q] * f2[q], k3 = h[q] * f3[q], k4 = h[q] * f4[q],
+                        k5 = h[q] * f5[q], k6 = h[q] * f6[q];
+            float er = kE[0] * k0;
+            er = __builtin_fmaf(kE[2], k2, er);
+            er = __builtin_fmaf(kE[3], k3, er);
+            er = __builtin_fmaf(kE[4], k4, er);
+            er = __builtin_fmaf(kE[5], k5, er);
+            er = __builtin_fmaf(kE[6], k6, er);
+            const float a0 = fabsf(y0[q]), a1 = fabsf(y1[q]);
+            const float mx = a0 > a1 ? a0 : a1;
+            const float den = p.atol + mx * p.rtol;
+            const float qe = er / den;
+            part[q] = part[q] + qe * qe;
+            float acc = kM[0] * k0;
+            acc = __builtin_fmaf(kM[2], k2, acc);
+            acc = __builtin_fmaf(kM[3], k3, acc);
+            acc = __builtin_fmaf(kM[4], k4, acc);
+            acc = __builtin_fmaf(kM[5], k5, acc);
+            acc = __builtin_fmaf(kM[6], k6, acc);
+            const float yy0 = y0[q], yy1 = y1[q];
+            const float ym = yy0 + acc;
+            ca[q] = ((2.0f * (k6 - k0)) - (8.0f * (yy1 + yy0))) + (16.0f * ym);
+            cb[q] = ((((5.0f * k0) - (3.0f * k6)) + (18.0f * yy0)) + (14.0f * yy1)) - (32.0f * ym);
+            cc[q] = (((k6 - (4.0f * k0)) - (11.0f * yy0)) - (5.0f * yy1)) + (16.0f * ym);
+        }
+        store8(ws, SL_CA, i, hq, ca);
+        store8(ws, SL_CB, i, hq, cb);
+        store8(ws, SL_CC, i, hq, cc);
+    }
+    rm_publish(part);
+    __syncthreads();
+    // (2) thread e: accept/reject, step-size update (diffrax PIDController)
+    if (tid < E_WG) {
+        CtlE& c = s_ctl[tid];
+        c.nsave = 0;
+        c.keep = 0;
+        if (c.active) {
+            const float mean = rm_total(tid) / (float)N;
+            const float err = sqrtf(mean);
+            const bool keep = err < 1.0f;
+            float fac = 0.9f * kdm_inv_fifth_root(err);
+            const float fmn = keep ? 1.0f : 0.2f;
+            fac = fac > fmn ? fac : fmn;
+            fac = fac < 10.0f ? fac : 10.0f;
+            c.dtn = c.h * fac;
+            c.keep = keep;
+            if (keep) {
+                int k = 0;
+                while (c.si + k < c.n && (float)grid_at_c(c, c.si + k) <= c.tnext) ++k;
+                c.nsave = k;
             }
-            if (c.si >= c.lfp_from && c.si < c.lfp_to) {
-                float ln;
-                double lr;
-                lfp_of_row<EPL>(p, env, row, &ln, &lr);
-                const int pos = c.si - c.lfp_from + c.pos0;
-                if (lane == 0) {
-                    if (to_ring) {
-                        p.ring[(size_t)env * p.W + pos] = lr;
-                    } else {
-                        s_smp_n[e][pos] = ln;
-                        s_smp_r[e][pos] = lr;
+        }
+    }
+    __syncthreads();
+    if (tid == 0) {
+        int m = 0;
+        for (int e = 0; e < E_WG; ++e) m = s_ctl[e].nsave > m ? s_ctl[e].nsave : m;
+        s_maxsave = m;
+    }
+    __syncthreads();
+    const int nrounds = s_maxsave;
+    // (3) saves: one round per save index, all envs in parallel
+#pragma unroll 1
+    for (int r = 0; r < nrounds; ++r) {
+        if (tid < E_WG) {
+            const CtlE& c = s_ctl[tid];
+            int fl = 0;
+            float th = 0.0f;
+            if (r < c.nsave) {
+                const int si = c.si + r;
+                const float ts = (float)grid_at_c(c, si);
+                th = (ts - c.tprev) / (c.tnext - c.tprev);
+                fl = 1 | ((si >= c.lfp_from && si < c.lfp_to) ? 2 : 0) | ((si == c.n - 1) ? 4 : 0);
+            }
+            s_theta[tid] = th;
+            s_rflag[tid] = fl;
+        }
+        __syncthreads();
+        float th[8];
+        int fl[8];
+        int anyl = 0, anyf = 0;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            th[q] = s_theta[mfma_env(q, lane)];
+            fl[q] = s_rflag[mfma_env(q, lane)];
+            anyl |= fl[q] & 2;
+            anyf |= fl[q] & 4;
+        }
+        float pn[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        double pg[4][8];
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr)
+#pragma unroll
+            for (int q = 0; q < 8; ++q) pg[rr][q] = 0.0;
+        const bool gauss = p.rec_kernel == KURA_REC_GAUSSIAN;
+#pragma unroll 1
+        for (int t = 0; t < TPW; ++t) {
+            const int i = 32 * (wave * TPW + t) + (lane & 31);
+            float ca[8], cb[8], cc[8], f0[8], y0[8];
+            load8(ws, SL_CA, i, hq, ca);
+            load8(ws, SL_CB, i, hq, cb);
+            load8(ws, SL_CC, i, hq, cc);
+            load8(ws, SL_F0, i, hq, f0);
+            load8(ws, SL_Y0, i, hq, y0);
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                const float k0 = h[q] * f0[q];
+                float v = ca[q] * th[q] + cb[q];
+                v = v * th[q] + cc[q];
+                v = v * th[q] + k0;
+                v = v * th[q] + y0[q];
+                const int env = env_base + mfma_env(q, lane);
+                if (fl[q] & 2) {
+                    const float cr = kdm_cosf(v);
+                    pn[q] = pn[q] + cr;
+                    if (gauss) {
+                        const int ge = env < p.B ? env : p.B - 1;
+#pragma unroll
+                        for (int rr = 0; rr < 4; ++rr)
+                            if (rr < p.n_rec)
+                                pg[rr][q] = pg[rr][q] + (double)cr * p.g_rec[((size_t)ge * p.n_rec + rr) * N + i];
                     }
                 }
+                if ((fl[q] & 4) && env < p.B) p.y[(size_t)env * N + i] = v;
             }
-            if (c.si == c.g.n - 1) {
+        }
+        (void)anyf;
+        if (__any(anyl)) {  // identical in every wave: each wave holds all 16 envs
+            rm_publish(pn);
+            if (gauss) {
 #pragma unroll
-                for (int m = 0; m < EPL; ++m) p.y[(size_t)env * N + lane + 64 * m] = row[m];
+                for (int rr = 0; rr < 4; ++rr)
+                    if (rr < p.n_rec) rm_publish_d(pg[rr], rr);
             }
-            c.si++;
         }
-        // y0 <- y1, f0 <- f6 (FSAL)
-        float2* rec2 = reinterpret_cast<float2*>(p.R + (size_t)env * N * 8) + 4 * lane;
+        __syncthreads();
+        if (tid < E_WG && (s_rflag[tid] & 2)) {
+            const CtlE& c = s_ctl[tid];
+            const int si = c.si + r;
+            const float ln = rm_total(tid) / (float)N;
+            double lr = (double)ln;
+            if (gauss) {
+                double acc = 0.0;
+                for (int rr = 0; rr < p.n_rec; ++rr) acc = acc + rm_total_d(tid, rr) / (double)N;
+                lr = acc;
+            }
+            const int pos = si - c.lfp_from + c.pos0;
+            if (to_ring) {
+                p.ring[(size_t)(env_base + tid) * p.W + pos] = lr;
+            } else {
+                s_smp_n[tid][pos] = ln;
+                s_smp_r[tid][pos] = lr;
+            }
+        }
+        __syncthreads();
+    }
+    // (4) accepted envs: y0 <- y1, f0 <- f6 (FSAL)
+    int kp[8];
 #pragma unroll
-        for (int m = 0; m < EPL; ++m) {
-            const float f6 = p.R[((size_t)env * N + lane + 64 * m) * 8 + 7];
-            rec2[4 * 64 * m] = make_float2(y1p[64 * m], f6);
+    for (int q = 0; q < 8; ++q) kp[q] = s_ctl[mfma_env(q, lane)].keep;
+#pragma unroll 1
+    for (int t = 0; t < TPW; ++t) {
+        const int i = 32 * (wave * TPW + t) + (lane & 31);
+        float y0[8], y1[8], f0[8], f6[8];
+        load8(ws, SL_Y0, i, hq, y0);
+        load8(ws, SL_Y1, i, hq, y1);
+        load8(ws, SL_F0, i, hq, f0);
+        load8(ws, SL_F0 + 6, i, hq, f6);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            y0[q] = kp[q] ? y1[q] : y0[q];
+            f0[q] = kp[q] ? f6[q] : f0[q];
         }
-        c.tprev = c.tnext;
-    } else {
-        c.rejected++;
+        store8(ws, SL_Y0, i, hq, y0);
+        store8(ws, SL_F0, i, hq, f0);
     }
-    float tn = c.tprev + dtn;
-    c.tprev = fminf(c.tprev, c.t1);
-    if (tn > c.t1 - 1e-6f) tn = keep ? c.t1 : c.tprev + 0.5f * (c.t1 - c.tprev);
-    c.tnext = tn;
-    c.nsteps++;
-    if (!(c.tprev < c.t1)) c.active = 0;
-    if (c.active && c.nsteps >= p.max_steps) {
-        c.flags |= 1;
-        c.active = 0;
+    // (5) thread e: time advance (adapt_step_size + _clip_to_end)
+    __syncthreads();
+    if (tid < E_WG) {
+        CtlE& c = s_ctl[tid];
+        if (c.active) {
+            c.si += c.nsave;
+            if (c.keep) c.tprev = c.tnext;
+            else c.rejected++;
+            float tn = c.tprev + c.dtn;
+            c.tprev = fminf(c.tprev, c.t1);
+            if (tn > c.t1 - 1e-6f) tn = c.keep ? c.t1 : c.tprev + 0.5f * (c.t1 - c.tprev);
+            c.tnext = tn;
+            c.nsteps++;
+            if (!(c.tprev < c.t1)) c.active = 0;
+            if (c.active && c.nsteps >= p.max_steps) {
+                c.flags |= 1;
+                c.active = 0;
+            }
+        }
     }
+    __syncthreads();
 }
 
-// One diffeqsolve for the workgroup's envs (each wave drives its 2 envs'
-// control; the coupling GEMM always covers all 16 rows).
+// One diffeqsolve for the workgroup's 16 envs.  s_ctl must be initialised
+// (ctl_begin) and visible before the call.
 template <int TPW>
-__device__ void solve_wg(const DevParams& p, float* Xs, Ctl (&ctl)[ENVS_PER_WAVE], int env_base, bool to_ring,
-                         bool pulse_on, long long* rhs_count) {
-    constexpr int EPL = TPW * 4;  // N / 64
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+__device__ void solve_wg(const DevParams& p, float* Xs, int env_base, bool to_ring, bool pulse_on,
+                         long long* rhs_count) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, tid = threadIdx.x;
+    const int hq = lane >> 5;
     constexpr int N = TPW * 256;
-    // record.y0 <- state y for active envs
+    const Slot ws{p.R + (size_t)blockIdx.x * NSLOT * N * 16, N};
+    // record y0 <- state y (MFMA layout)
 #pragma unroll 1
-    for (int ee = 0; ee < ENVS_PER_WAVE; ++ee) {
-        const int env = env_base + wave * ENVS_PER_WAVE + ee;
-        if (env >= p.B || !ctl[ee].active) continue;
+    for (int t = 0; t < TPW; ++t) {
+        const int i = 32 * (wave * TPW + t) + (lane & 31);
+        float v[8];
 #pragma unroll
-        for (int m = 0; m < EPL; ++m) {
-            const size_t o = (size_t)env * N + lane + 64 * m;
-            p.R[o * 8] = p.y[o];
+        for (int q = 0; q < 8; ++q) {
+            const int env = env_base + mfma_env(q, lane);
+            v[q] = env < p.B ? p.y[(size_t)env * N + i] : 0.0f;
         }
+        store8(ws, SL_Y0, i, hq, v);
     }
-    __syncthreads();  // pulse / records written above are visible to every lane
     STAMP_DECL
     long long nrhs = 0;
     int s = 0;  // stage 0 = initial RHS at y0 (FSAL seed)
     for (;;) {
         floatx16 acc[TPW];
         EpiConst<TPW> kc;
-        stage_input<EPL>(p, Xs, ctl, env_base, s);
+        stage_input<TPW>(ws, Xs, s);
         STAMP(0);
         load_epi_const<TPW>(p, env_base, pulse_on, kc);
         __syncthreads();
         STAMP(1);
         coupling_gemm<TPW>(Xs, p.alpha_sw, acc);
         STAMP(2);
-        coupling_epilogue<TPW>(p, Xs, acc, kc, env_base, s);
+        coupling_epilogue<TPW>(p, ws, Xs, acc, kc, s);
         STAMP(3);
         __syncthreads();
         STAMP(4);
@@ -499,67 +676,51 @@ __device__ void solve_wg(const DevParams& p, float* Xs, Ctl (&ctl)[ENVS_PER_WAVE
             continue;
         }
         if (s == 6) {
-#pragma unroll 1
-            for (int ee = 0; ee < ENVS_PER_WAVE; ++ee) {
-                const int e = wave * ENVS_PER_WAVE + ee;
-                const int env = env_base + e;
-                if (env >= p.B || !ctl[ee].active) continue;
-                post_step<EPL>(p, ctl[ee], env, e, to_ring);
-            }
+            post_step<TPW>(p, ws, env_base, to_ring);
             STAMP(5);
         }
-        // workgroup-wide "any env still integrating?"
-        if (threadIdx.x == 0) s_wg_flag = 0;
-        __syncthreads();
-        int mine = 0;
-#pragma unroll
-        for (int ee = 0; ee < ENVS_PER_WAVE; ++ee) mine |= ctl[ee].active;
-        if (mine && lane == 0) atomicOr(&s_wg_flag, 1);
-        __syncthreads();
-        const int any = s_wg_flag;
+        if (tid == 0) {
+            int any = 0;
+            for (int e = 0; e < E_WG; ++e) any |= s_ctl[e].active;
+            s_any = any;
+            for (int e = 0; e < E_WG; ++e)
+                if (s_ctl[e].active) s_ctl[e].h = s_ctl[e].tnext - s_ctl[e].tprev;
+        }
         __syncthreads();
         STAMP(6);
-        if (any == 0) break;
-#pragma unroll
-        for (int ee = 0; ee < ENVS_PER_WAVE; ++ee)
-            if (ctl[ee].active) ctl[ee].h = ctl[ee].tnext - ctl[ee].tprev;
+        if (s_any == 0) break;
         s = 1;
     }
     STAMP_FLUSH(p);
     *rhs_count += nrhs;
 }
 
-__device__ __forceinline__ void ctl_begin(Ctl& c, const Grid& g, float dt0, int lfp_from, int lfp_to, int pos0) {
-    c.g = g;
-    const float t0 = (float)grid_at(g, 0);
-    c.t1 = (float)grid_at(g, g.n - 1);
-    c.tprev = t0;
-    c.tnext = fminf(t0 + dt0, c.t1);
-    c.h = 0.0f;
-    c.si = 0;
-    c.nsteps = 0;
-    c.lfp_from = lfp_from;
-    c.lfp_to = lfp_to;
-    c.pos0 = pos0;
-    c.active = g.n >= 2;
-}
-
-__device__ __forceinline__ void flush_stats(const DevParams& p, long long rhs, const Ctl (&ctl)[ENVS_PER_WAVE],
-                                            int env_base) {
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    if (lane != 0) return;
+__device__ __forceinline__ void flush_stats(const DevParams& p, long long rhs, int env_base) {
+    if (threadIdx.x != 0) return;
     unsigned long long steps = 0, rej = 0, flags = 0;
-#pragma unroll
-    for (int ee = 0; ee < ENVS_PER_WAVE; ++ee) {
-        if (env_base + wave * ENVS_PER_WAVE + ee >= p.B) continue;
-        steps += ctl[ee].nsteps;
-        rej += ctl[ee].rejected;
-        flags |= ctl[ee].flags;
+    for (int e = 0; e < E_WG; ++e) {
+        if (env_base + e >= p.B) continue;
+        steps += s_ctl[e].acc_steps + s_ctl[e].nsteps;
+        rej += s_ctl[e].acc_rej + s_ctl[e].rejected;
+        flags |= s_ctl[e].flags;
     }
-    if (wave == 0) atomicMax(&p.stats[0], (unsigned long long)rhs);
+    atomicMax(&p.stats[0], (unsigned long long)rhs);
     atomicAdd(&p.stats[1], steps);
     atomicAdd(&p.stats[2], rej);
     if (flags) atomicOr(&p.stats[3], flags);
+}
+
+// Kernel prologue: zero every env's control slot.
+__device__ __forceinline__ void ctl_clear() {
+    if (threadIdx.x < E_WG) {
+        CtlE& c = s_ctl[threadIdx.x];
+        c.active = 0;
+        c.nsteps = c.rejected = c.flags = 0;
+        c.acc_steps = c.acc_rej = 0;
+        c.n = 0;
+        c.h = 0.0f;
+        c.keep = c.nsave = 0;
+    }
 }
 
 // R64 dot of the window (lane-strided, registers) with a twiddle row.
@@ -681,93 +842,81 @@ __global__ __launch_bounds__(NTHREADS) void kura_step_kernel(DevParams p, const 
                                                              uint8_t* __restrict__ done, float* __restrict__ lfp_true,
                                                              double* __restrict__ lfp_rec, int* __restrict__ nsamp) {
     extern __shared__ float Xs[];  // xs_floats(N)
-    constexpr int EPL = TPW * 4;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    __shared__ int s_nI[E_WG], s_nII[E_WG];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, tid = threadIdx.x;
     const int N = p.N;
     const int env_base = blockIdx.x * E_WG;
-    Ctl ctl[ENVS_PER_WAVE];
-    double u0v[ENVS_PER_WAVE];
-    int nI[ENVS_PER_WAVE], nII[ENVS_PER_WAVE], steps[ENVS_PER_WAVE], rej[ENVS_PER_WAVE], flg[ENVS_PER_WAVE];
-    // ---- stimulation ON: pulse = float32(sum_e g_e * u_e)  (env.py:419-424)
-#pragma unroll
-    for (int ee = 0; ee < ENVS_PER_WAVE; ++ee) {
-        const int env = env_base + wave * ENVS_PER_WAVE + ee;
-        ctl[ee].active = 0;
-        ctl[ee].rejected = 0;
-        ctl[ee].flags = 0;
-        ctl[ee].nsteps = 0;
-        nI[ee] = 0;
-        nII[ee] = 0;
-        u0v[ee] = 0.0;
-        if (env >= p.B) continue;
-        double u[4] = {0.0, 0.0, 0.0, 0.0};
-        const int ne = p.n_elec < 4 ? p.n_elec : 4;
-        for (int e = 0; e < ne; ++e) {
-            const double a = (double)action[(size_t)env * p.n_elec + e];
-            u[e] = p.dbs_lo + ((p.dbs_hi - p.dbs_lo) * (a - p.act_lo)) / (p.act_hi - p.act_lo);
-        }
-        u0v[ee] = u[0];
-        for (int m = 0; m < EPL; ++m) {
-            const int i = lane + 64 * m;
-            double pacc = 0.0;
-            for (int e = 0; e < ne; ++e) pacc = pacc + p.g_stim[((size_t)env * p.n_elec + e) * N + i] * u[e];
-            p.pulse[(size_t)env * N + i] = (float)pacc;
-        }
-        const double t = p.t[env];
-        const Grid g = make_grid(t, t + p.width, p.dt);
-        nI[ee] = g.n;
-        ctl_begin(ctl[ee], g, p.dt0, 0, g.n, 0);
-        if (g.n < 2 || g.n > KURA_S_MAX) {
-            ctl[ee].active = 0;
-            ctl[ee].flags |= 8;
+    ctl_clear();
+    // ---- thread e: rescale_action (env.py:389-393), ON grid (env.py:426-428)
+    if (tid < E_WG) {
+        const int env = env_base + tid;
+        s_nI[tid] = s_nII[tid] = 0;
+        for (int k = 0; k < 4; ++k) s_u[tid][k] = 0.0;
+        if (env < p.B) {
+            const int ne = p.n_elec < 4 ? p.n_elec : 4;
+            for (int k = 0; k < ne; ++k) {
+                const double a = (double)action[(size_t)env * p.n_elec + k];
+                s_u[tid][k] = p.dbs_lo + ((p.dbs_hi - p.dbs_lo) * (a - p.act_lo)) / (p.act_hi - p.act_lo);
+            }
+            const double t = p.t[env];
+            const Grid g = make_grid(t, t + p.width, p.dt);
+            s_nI[tid] = g.n;
+            ctl_begin(s_ctl[tid], g, p.dt0, 0, g.n, 0);
+            if (g.n < 2 || g.n > KURA_S_MAX) {
+                s_ctl[tid].active = 0;
+                s_ctl[tid].flags |= 8;
+            }
         }
     }
-    long long rhs = 0;
     __syncthreads();
-    solve_wg<TPW>(p, Xs, ctl, env_base, false, true, &rhs);
-    // ---- stimulation OFF (env.py:433-441)
-#pragma unroll
+    // ---- pulse = float32(sum_e g_e * u_e) for the envs of this wave (env.py:419-424)
+#pragma unroll 1
     for (int ee = 0; ee < ENVS_PER_WAVE; ++ee) {
         const int e = wave * ENVS_PER_WAVE + ee;
         const int env = env_base + e;
-        steps[ee] = ctl[ee].nsteps;
-        rej[ee] = ctl[ee].rejected;
-        flg[ee] = ctl[ee].flags;
-        ctl[ee].active = 0;
-        if (env >= p.B || flg[ee]) continue;
-        for (int m = 0; m < EPL; ++m) p.pulse[(size_t)env * N + lane + 64 * m] = 0.0f;
-        const double tm = grid_at(ctl[ee].g, nI[ee] - 1);
-        const Grid g = make_grid(tm, tm + p.pause, p.dt);
-        nII[ee] = g.n;
-        ctl_begin(ctl[ee], g, p.dt0, 1, g.n - 1, nI[ee] + 1);
-        ctl[ee].rejected = 0;
-        ctl[ee].flags = 0;
-        if (g.n < 2 || nI[ee] + g.n - 1 > KURA_S_MAX) {
-            ctl[ee].active = 0;
-            flg[ee] |= 8;
-        }
-        if (lane == 0) {  // ys_II[0] == ys_I[-1]: duplicated sample (env.py:440)
-            s_smp_n[e][nI[ee]] = s_smp_n[e][nI[ee] - 1];
-            s_smp_r[e][nI[ee]] = s_smp_r[e][nI[ee] - 1];
+        if (env >= p.B) continue;
+        const int ne = p.n_elec < 4 ? p.n_elec : 4;
+        for (int i = lane; i < N; i += 64) {
+            double pacc = 0.0;
+            for (int k = 0; k < ne; ++k) pacc = pacc + p.g_stim[((size_t)env * p.n_elec + k) * N + i] * s_u[e][k];
+            p.pulse[(size_t)env * N + i] = (float)pacc;
         }
     }
-    solve_wg<TPW>(p, Xs, ctl, env_base, false, false, &rhs);
     __syncthreads();
-    // ---- window, reward, outputs (env.py:443-454)
+    long long rhs = 0;
+    solve_wg<TPW>(p, Xs, env_base, false, true, &rhs);
+    // ---- stimulation OFF (env.py:433-441)
+    if (tid < E_WG) {
+        CtlE& c = s_ctl[tid];
+        const int env = env_base + tid;
+        c.active = 0;
+        if (env < p.B && !c.flags) {
+            const int nI = s_nI[tid];
+            const double tm = grid_at_c(c, nI - 1);
+            const Grid g = make_grid(tm, tm + p.pause, p.dt);
+            s_nII[tid] = g.n;
+            ctl_begin(c, g, p.dt0, 1, g.n - 1, nI + 1);
+            if (g.n < 2 || nI + g.n - 1 > KURA_S_MAX) {
+                c.active = 0;
+                c.flags |= 8;
+            } else {  // ys_II[0] == ys_I[-1]: duplicated sample (env.py:440)
+                s_smp_n[tid][nI] = s_smp_n[tid][nI - 1];
+                s_smp_r[tid][nI] = s_smp_r[tid][nI - 1];
+            }
+        }
+    }
+    __syncthreads();
+    solve_wg<TPW>(p, Xs, env_base, false, false, &rhs);
+    // ---- window, reward, outputs (env.py:443-454): wave w owns envs 2w, 2w+1
     constexpr int WPL = WPL_MAX;
 #pragma unroll 1
     for (int ee = 0; ee < ENVS_PER_WAVE; ++ee) {
         const int e = wave * ENVS_PER_WAVE + ee;
         const int env = env_base + e;
-        steps[ee] += ctl[ee].nsteps;
-        rej[ee] += ctl[ee].rejected;
-        flg[ee] |= ctl[ee].flags;
-        ctl[ee].nsteps = steps[ee];
-        ctl[ee].rejected = rej[ee];
-        ctl[ee].flags = flg[ee];
         if (env >= p.B) continue;
-        const int S = nI[ee] + nII[ee] - 1;
-        if (flg[ee] || S < 1) {
+        const CtlE& c = s_ctl[e];
+        const int S = s_nI[e] + s_nII[e] - 1;
+        if (c.flags || S < 1) {
             if (lane == 0) {
                 if (nsamp) nsamp[env] = 0;
                 if (done) done[env] = 1;
@@ -791,7 +940,7 @@ __global__ __launch_bounds__(NTHREADS) void kura_step_kernel(DevParams p, const 
         }
         double* ext = p.scratch + (size_t)env * 2 * (W + 2 * p.padlen);
         double* tmp = ext + (W + 2 * p.padlen);
-        const double r = reward_of<WPL>(p, x, u0v[ee], xv, ext, tmp);
+        const double r = reward_of<WPL>(p, x, s_u[e][0], xv, ext, tmp);
         // ring append after every read of the old slots
         if (lane < S) {
             int k = wp0 + lane;
@@ -804,7 +953,7 @@ __global__ __launch_bounds__(NTHREADS) void kura_step_kernel(DevParams p, const 
             p.wpos[env] = wp;
             const int st = p.step[env] + 1;
             p.step[env] = st;
-            p.t[env] = grid_at(ctl[ee].g, nII[ee] - 1);
+            p.t[env] = grid_at_c(c, s_nII[e] - 1);
             if (reward) reward[env] = r;
             if (done) done[env] = st >= p.episode_steps;
             if (nsamp) nsamp[env] = S;
@@ -814,7 +963,7 @@ __global__ __launch_bounds__(NTHREADS) void kura_step_kernel(DevParams p, const 
             if (lfp_rec) lfp_rec[(size_t)env * KURA_S_MAX + lane] = lane < S ? s_smp_r[e][lane] : 0.0;
         }
     }
-    flush_stats(p, rhs, ctl, env_base);
+    flush_stats(p, rhs, env_base);
 }
 
 // ----------------------------------------------------------- reset kernel --
@@ -823,44 +972,41 @@ __global__ __launch_bounds__(NTHREADS) void kura_reset_kernel(DevParams p, const
                                                               const float* __restrict__ theta0,
                                                               float* __restrict__ obs) {
     extern __shared__ float Xs[];
-    constexpr int EPL = TPW * 4;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int N = p.N;
-    const int W = p.W;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, tid = threadIdx.x;
+    const int N = p.N, W = p.W;
     const int env_base = blockIdx.x * E_WG;
-    Ctl ctl[ENVS_PER_WAVE];
-#pragma unroll
-    for (int ee = 0; ee < ENVS_PER_WAVE; ++ee) {
-        const int env = env_base + wave * ENVS_PER_WAVE + ee;
-        ctl[ee].active = 0;
-        ctl[ee].rejected = 0;
-        ctl[ee].flags = 0;
-        ctl[ee].nsteps = 0;
-        if (env >= p.B || (mask && !mask[env])) continue;
-        for (int m = 0; m < EPL; ++m) {
-            const size_t o = (size_t)env * N + lane + 64 * m;
-            p.y[o] = theta0[o];
-            p.pulse[o] = 0.0f;
+    ctl_clear();
+    if (tid < E_WG) {
+        const int env = env_base + tid;
+        if (env < p.B && (!mask || mask[env])) {
+            const Grid g = make_grid(0.0, p.transient_len, p.dt);
+            ctl_begin(s_ctl[tid], g, p.dt0, g.n - 1 - W, g.n - 1, 0);
         }
-        const Grid g = make_grid(0.0, p.transient_len, p.dt);
-        ctl_begin(ctl[ee], g, p.dt0, g.n - 1 - W, g.n - 1, 0);
     }
-    long long rhs = 0;
-    solve_wg<TPW>(p, Xs, ctl, env_base, true, false, &rhs);
-    __syncthreads();
-#pragma unroll
+    // state y <- theta0 for the masked envs
+#pragma unroll 1
     for (int ee = 0; ee < ENVS_PER_WAVE; ++ee) {
         const int env = env_base + wave * ENVS_PER_WAVE + ee;
+        if (env >= p.B || (mask && !mask[env])) continue;
+        for (int i = lane; i < N; i += 64) p.y[(size_t)env * N + i] = theta0[(size_t)env * N + i];
+    }
+    __syncthreads();
+    long long rhs = 0;
+    solve_wg<TPW>(p, Xs, env_base, true, false, &rhs);
+#pragma unroll 1
+    for (int ee = 0; ee < ENVS_PER_WAVE; ++ee) {
+        const int e = wave * ENVS_PER_WAVE + ee;
+        const int env = env_base + e;
         if (env >= p.B || (mask && !mask[env])) continue;
         if (lane == 0) {
-            p.t[env] = grid_at(ctl[ee].g, ctl[ee].g.n - 1);
+            p.t[env] = grid_at_c(s_ctl[e], s_ctl[e].n - 1);
             p.step[env] = 0;
             p.wpos[env] = 0;
         }
         if (obs)
             for (int i = lane; i < W; i += 64) obs[(size_t)env * W + i] = (float)p.ring[(size_t)env * W + i];
     }
-    flush_stats(p, rhs, ctl, env_base);
+    flush_stats(p, rhs, env_base);
 }
 
 // ------------------------------------------------------ standalone reward --

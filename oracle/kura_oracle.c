@@ -98,6 +98,50 @@ double oracle_r64_f64(const double* x, int n) {
     return p[0];
 }
 
+/* RM: the order of every per-env sum over the N oscillators inside the solver
+ * (error norm, LFP).  It is the order in which the HIP kernel reduces in the
+ * MFMA accumulator layout: wave w (0..7) owns columns 32*(w*TPW + t) + c
+ * (TPW = N/256 column tiles, c = 0..31); per column lane c the TPW values are
+ * summed in t order, the 32 lanes combine by an xor butterfly (16,8,4,2,1),
+ * and the 8 wave totals are added in wave order from +0. */
+float oracle_rm_f32(const float* x, int n) {
+    const int tpw = n / 256;
+    float tot = 0.0f;
+    for (int w = 0; w < 8; ++w) {
+        float p[32], q[32];
+        for (int c = 0; c < 32; ++c) {
+            float a = 0.0f;
+            for (int t = 0; t < tpw; ++t) a = a + x[32 * (w * tpw + t) + c];
+            p[c] = a;
+        }
+        for (int o = 16; o >= 1; o >>= 1) {
+            for (int c = 0; c < 32; ++c) q[c] = p[c] + p[c ^ o];
+            memcpy(p, q, sizeof(p));
+        }
+        tot = tot + p[0];
+    }
+    return tot;
+}
+
+double oracle_rm_f64(const double* x, int n) {
+    const int tpw = n / 256;
+    double tot = 0.0;
+    for (int w = 0; w < 8; ++w) {
+        double p[32], q[32];
+        for (int c = 0; c < 32; ++c) {
+            double a = 0.0;
+            for (int t = 0; t < tpw; ++t) a = a + x[32 * (w * tpw + t) + c];
+            p[c] = a;
+        }
+        for (int o = 16; o >= 1; o >>= 1) {
+            for (int c = 0; c < 32; ++c) q[c] = p[c] + p[c ^ o];
+            memcpy(p, q, sizeof(p));
+        }
+        tot = tot + p[0];
+    }
+    return tot;
+}
+
 static double r64_dot_f64(const double* x, const double* w, int n) {
     double p[64];
     for (int l = 0; l < 64; ++l) {
@@ -241,14 +285,14 @@ static void rhs(const OCtx* o, Work* w, const float* y, const float* omega, cons
 static void lfp_row(const OCtx* o, Work* w, const float* row, const double* g_rec, float* naive, double* rec) {
     const int N = o->N;
     for (int j = 0; j < N; ++j) w->cosrow[j] = kdm_cosf(row[j]);
-    float m = oracle_r64_f32(w->cosrow, N) / (float)N;
+    float m = oracle_rm_f32(w->cosrow, N) / (float)N;
     *naive = m;
     if (o->cfg.rec_kernel == KURA_REC_GAUSSIAN) {
         double acc = 0.0;
         for (int r = 0; r < o->cfg.n_rec; ++r) {
             const double* g = g_rec + (size_t)r * N;
             for (int j = 0; j < N; ++j) w->prod[j] = (double)w->cosrow[j] * g[j];
-            acc = acc + oracle_r64_f64(w->prod, N) / (double)N;
+            acc = acc + oracle_rm_f64(w->prod, N) / (double)N;
         }
         *rec = acc;
     } else {
@@ -339,7 +383,7 @@ static void solve(const OCtx* o, Work* w, const Grid* g, float* y_start, const f
             float q = e / den;
             w->cosrow[i] = q * q; /* scratch */
         }
-        float mean = oracle_r64_f32(w->cosrow, N) / (float)N;
+        float mean = oracle_rm_f32(w->cosrow, N) / (float)N;
         float err = sqrtf(mean);
         int keep = err < 1.0f;
         float fac = 0.9f * kdm_inv_fifth_root(err);
