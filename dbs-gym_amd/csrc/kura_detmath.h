@@ -50,17 +50,15 @@
 // classic shift-subtract path, which is exact by Sterbenz's lemma.
 KDM_FN float kdm_fmod2pi(float y) {
     const float d = KDM_TWO_PI_F;
-    float ay = y < 0.0f ? -y : y;
-    float r;
-    if (ay < 4194304.0f) {
-        float q = truncf(ay * KDM_INV_TWO_PI_F);
-        r = KDM_FMAF(-q, d, ay);
-        if (r < 0.0f) r += d;
-        else if (r >= d) r -= d;
-    } else {
+    const float ay = fabsf(y);
+    // fast path (|y| < 2^22), branch-free: exact remainder by fmaf, one fix-up
+    const float q = truncf(ay * KDM_INV_TWO_PI_F);
+    float r = KDM_FMAF(-q, d, ay);
+    r = r < 0.0f ? r + d : r;
+    r = r >= d ? r - d : r;
+    if (!(ay < 4194304.0f)) {  // rare: shift-subtract long division
         r = ay;
         if (!(r < 3.0e38f)) return (y - y) / (y - y);  // inf/nan -> nan
-        // scale d up by powers of two until just below r, then subtract down
         float dd = d;
         int e = 0;
         while (dd * 2.0f <= r) { dd *= 2.0f; ++e; }
@@ -87,13 +85,12 @@ KDM_FN void kdm_sincosf(float x, float* s_out, float* c_out) {
     float pc = KDM_FMAF(z, 2.443315711809948e-5f, -1.388731625493765e-3f);
     pc = KDM_FMAF(z, pc, 4.166664568298827e-2f);
     float cr = KDM_FMAF(z * z, pc, KDM_FMAF(-0.5f, z, 1.0f));
-    float s, c;
-    switch (q) {
-        case 0: s = sr; c = cr; break;
-        case 1: s = cr; c = -sr; break;
-        case 2: s = -sr; c = -cr; break;
-        default: s = -cr; c = sr; break;
-    }
+    // quadrant selection without branches (v_cndmask on the GPU):
+    // q=0: (s,c) = (sr,cr); 1: (cr,-sr); 2: (-sr,-cr); 3: (-cr,sr)
+    float s = (q & 1) ? cr : sr;
+    float c = (q & 1) ? sr : cr;
+    s = (q & 2) ? -s : s;
+    c = ((q + 1) & 2) ? -c : c;
     *s_out = s;
     *c_out = c;
 }

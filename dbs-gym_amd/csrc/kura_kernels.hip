@@ -74,7 +74,7 @@ struct DevParams {
     const float* alpha_sw;  // B-fragment swizzled coupling
     const float* omega;     // [B][N]
     const double* g_stim;   // [B][n_elec][N]
-    const double* g_rec;    // [B][n_rec][N]
+    const double* g_rec;    // [B][N] recorder conductance sum G = g_0 + g_1 + ... (host-summed)
     const double* ctab;     // [n_bins][W]
     const double* stab;
     float* y;               // [B][N] phase state (last saved row)
@@ -212,10 +212,11 @@ struct CtlE {
     float t1, tprev, tnext, h, dtn;
 };
 __shared__ CtlE s_ctl[E_WG];
-__shared__ float s_red[NWAVES][E_WG];            // per-wave partial sums (f32)
-__shared__ double s_redd[NWAVES][E_WG][4];       // per-wave partial sums (f64, per recorder)
-__shared__ float s_theta[E_WG];                  // dense-output abscissa of this save round
-__shared__ int s_rflag[E_WG];                    // bit0: save row, bit1: LFP row, bit2: final row
+#define RC 4  // save rounds evaluated per pass over the records
+__shared__ float s_red[RC][NWAVES][E_WG];        // per-wave partial sums (f32)
+__shared__ double s_redd[RC][NWAVES][E_WG];      // per-wave partial sums (f64, recorder LFP)
+__shared__ float s_theta[E_WG][RC];              // dense-output abscissae of the rounds of a pass
+__shared__ int s_rflag[E_WG][RC];                // bit0: save row, bit1: LFP row, bit2: final row
 __shared__ double s_u[E_WG][4];                  // rescaled amplitudes (env.py:389-393)
 __shared__ int s_maxsave, s_any;
 
@@ -330,34 +331,37 @@ __device__ __forceinline__ void coupling_epilogue(const DevParams& p, const Slot
 
 // Stage input ys = y0 + chain_j(A[s][j] * h*f_j) (zero coefficients skipped,
 // as in the oracle), theta = fmod(ys, 2pi), sin/cos into the LDS operand.
-// Stage 0 is the solve's initial RHS at y0.
-template <int TPW>
-__device__ __forceinline__ void stage_input(const Slot& ws, float* Xs, int s) {
+// Stage 0 is the solve's initial RHS at y0.  Column tiles are processed two at
+// a time so the records of both are in flight before any use.
+template <int NT>
+__device__ __forceinline__ void stage_tiles(const Slot& ws, float* Xs, int s, const float (&h)[8], int t0) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int hq = lane >> 5;
-    float h[8];
+    const int TPW = ws.N / 256;
+    float y0[NT][8], f[NT][6][8];
 #pragma unroll
-    for (int q = 0; q < 8; ++q) h[q] = s_ctl[mfma_env(q, lane)].h;
-#pragma unroll 1
-    for (int t = 0; t < TPW; ++t) {
-        const int i = 32 * (wave * TPW + t) + (lane & 31);
-        float y0[8], f[6][8];
-        load8(ws, SL_Y0, i, hq, y0);
+    for (int u = 0; u < NT; ++u) {
+        const int i = 32 * (wave * TPW + t0 + u) + (lane & 31);
+        load8(ws, SL_Y0, i, hq, y0[u]);
 #pragma unroll
         for (int j = 0; j < 6; ++j)
-            if (j < s) load8(ws, SL_F0 + j, i, hq, f[j]);
+            if (j < s) load8(ws, SL_F0 + j, i, hq, f[u][j]);
+    }
+#pragma unroll
+    for (int u = 0; u < NT; ++u) {
+        const int i = 32 * (wave * TPW + t0 + u) + (lane & 31);
         float ys[8];
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
-            float v = y0[q];
+            float v = y0[u][q];
             if (s > 0) {
-                float acc = cA[s][0] * (h[q] * f[0][q]);
-                if (s > 1 && cA[s][1] != 0.0f) acc = __builtin_fmaf(cA[s][1], h[q] * f[1][q], acc);
-                if (s > 2) acc = __builtin_fmaf(cA[s][2], h[q] * f[2][q], acc);
-                if (s > 3) acc = __builtin_fmaf(cA[s][3], h[q] * f[3][q], acc);
-                if (s > 4) acc = __builtin_fmaf(cA[s][4], h[q] * f[4][q], acc);
-                if (s > 5) acc = __builtin_fmaf(cA[s][5], h[q] * f[5][q], acc);
-                v = y0[q] + acc;
+                float acc = cA[s][0] * (h[q] * f[u][0][q]);
+                if (s > 1 && cA[s][1] != 0.0f) acc = __builtin_fmaf(cA[s][1], h[q] * f[u][1][q], acc);
+                if (s > 2) acc = __builtin_fmaf(cA[s][2], h[q] * f[u][2][q], acc);
+                if (s > 3) acc = __builtin_fmaf(cA[s][3], h[q] * f[u][3][q], acc);
+                if (s > 4) acc = __builtin_fmaf(cA[s][4], h[q] * f[u][4][q], acc);
+                if (s > 5) acc = __builtin_fmaf(cA[s][5], h[q] * f[u][5][q], acc);
+                v = y0[u][q] + acc;
             }
             ys[q] = v;
             float sn, cs;
@@ -370,39 +374,50 @@ __device__ __forceinline__ void stage_input(const Slot& ws, float* Xs, int s) {
     }
 }
 
+template <int TPW>
+__device__ __forceinline__ void stage_input(const Slot& ws, float* Xs, int s) {
+    const int lane = threadIdx.x & 63;
+    float h[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) h[q] = s_ctl[mfma_env(q, lane)].h;
+    constexpr int NT = TPW < 2 ? TPW : 2;
+#pragma unroll 1
+    for (int t = 0; t < TPW; t += NT) stage_tiles<NT>(ws, Xs, s, h, t);
+}
+
 // RM reduction (kura_detmath.h): per-lane partials (t order) -> 32-lane xor
-// butterfly -> s_red[wave][e]; the caller barriers, then thread e adds the
+// butterfly -> s_red[k][wave][e]; the caller barriers, then thread e adds the
 // 8 wave totals in wave order.
-__device__ __forceinline__ void rm_publish(const float (&part)[8]) {
+__device__ __forceinline__ void rm_publish(const float (&part)[8], int k) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
         float v = part[q];
 #pragma unroll
         for (int o = 16; o >= 1; o >>= 1) v = v + __shfl_xor(v, o, 64);
-        if ((lane & 31) == 0) s_red[wave][mfma_env(q, lane)] = v;
+        if ((lane & 31) == 0) s_red[k][wave][mfma_env(q, lane)] = v;
     }
 }
-__device__ __forceinline__ void rm_publish_d(const double (&part)[8], int r) {
+__device__ __forceinline__ void rm_publish_d(const double (&part)[8], int k) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
         double v = part[q];
 #pragma unroll
         for (int o = 16; o >= 1; o >>= 1) v = v + __shfl_xor(v, o, 64);
-        if ((lane & 31) == 0) s_redd[wave][mfma_env(q, lane)][r] = v;
+        if ((lane & 31) == 0) s_redd[k][wave][mfma_env(q, lane)] = v;
     }
 }
-__device__ __forceinline__ float rm_total(int e) {
+__device__ __forceinline__ float rm_total(int e, int k) {
     float tot = 0.0f;
 #pragma unroll
-    for (int w = 0; w < NWAVES; ++w) tot = tot + s_red[w][e];
+    for (int w = 0; w < NWAVES; ++w) tot = tot + s_red[k][w][e];
     return tot;
 }
-__device__ __forceinline__ double rm_total_d(int e, int r) {
+__device__ __forceinline__ double rm_total_d(int e, int k) {
     double tot = 0.0;
 #pragma unroll
-    for (int w = 0; w < NWAVES; ++w) tot = tot + s_redd[w][e][r];
+    for (int w = 0; w < NWAVES; ++w) tot = tot + s_redd[k][w][e];
     return tot;
 }
 
@@ -462,7 +477,7 @@ __device__ __forceinline__ void post_step(const DevParams& p, const Slot& ws, in
         store8(ws, SL_CB, i, hq, cb);
         store8(ws, SL_CC, i, hq, cc);
     }
-    rm_publish(part);
+    rm_publish(part, 0);
     __syncthreads();
     // (2) thread e: accept/reject, step-size update (diffrax PIDController)
     if (tid < E_WG) {
@@ -470,7 +485,7 @@ __device__ __forceinline__ void post_step(const DevParams& p, const Slot& ws, in
         c.nsave = 0;
         c.keep = 0;
         if (c.active) {
-            const float mean = rm_total(tid) / (float)N;
+            const float mean = rm_total(tid, 0) / (float)N;
             const float err = sqrtf(mean);
             const bool keep = err < 1.0f;
             float fac = 0.9f * kdm_inv_fifth_root(err);
@@ -494,97 +509,116 @@ __device__ __forceinline__ void post_step(const DevParams& p, const Slot& ws, in
     }
     __syncthreads();
     const int nrounds = s_maxsave;
-    // (3) saves: one round per save index, all envs in parallel
+    // (3) saves: RC rounds (save indices) per pass over the records, all envs
+    // in parallel; one RM reduction per round and LFP kind.
+    const bool gauss = p.rec_kernel == KURA_REC_GAUSSIAN;
 #pragma unroll 1
-    for (int r = 0; r < nrounds; ++r) {
+    for (int r0 = 0; r0 < nrounds; r0 += RC) {
         if (tid < E_WG) {
             const CtlE& c = s_ctl[tid];
-            int fl = 0;
-            float th = 0.0f;
-            if (r < c.nsave) {
-                const int si = c.si + r;
-                const float ts = (float)grid_at_c(c, si);
-                th = (ts - c.tprev) / (c.tnext - c.tprev);
-                fl = 1 | ((si >= c.lfp_from && si < c.lfp_to) ? 2 : 0) | ((si == c.n - 1) ? 4 : 0);
+            for (int k = 0; k < RC; ++k) {
+                const int r = r0 + k;
+                int fl = 0;
+                float th = 0.0f;
+                if (r < c.nsave) {
+                    const int si = c.si + r;
+                    const float ts = (float)grid_at_c(c, si);
+                    th = (ts - c.tprev) / (c.tnext - c.tprev);
+                    fl = 1 | ((si >= c.lfp_from && si < c.lfp_to) ? 2 : 0) | ((si == c.n - 1) ? 4 : 0);
+                }
+                s_theta[tid][k] = th;
+                s_rflag[tid][k] = fl;
             }
-            s_theta[tid] = th;
-            s_rflag[tid] = fl;
         }
         __syncthreads();
-        float th[8];
+        float th[RC][8];
         int fl[8];
-        int anyl = 0, anyf = 0;
+        int anyl = 0;
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
-            th[q] = s_theta[mfma_env(q, lane)];
-            fl[q] = s_rflag[mfma_env(q, lane)];
-            anyl |= fl[q] & 2;
-            anyf |= fl[q] & 4;
+            const int e = mfma_env(q, lane);
+            int f = 0;
+#pragma unroll
+            for (int k = 0; k < RC; ++k) {
+                th[k][q] = s_theta[e][k];
+                f |= s_rflag[e][k] << (3 * k);
+            }
+            fl[q] = f;
+            anyl |= f & 02222;
         }
-        float pn[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        double pg[4][8];
+        float pn[RC][8];
+        double pg[RC][8];
 #pragma unroll
-        for (int rr = 0; rr < 4; ++rr)
+        for (int k = 0; k < RC; ++k)
 #pragma unroll
-            for (int q = 0; q < 8; ++q) pg[rr][q] = 0.0;
-        const bool gauss = p.rec_kernel == KURA_REC_GAUSSIAN;
+            for (int q = 0; q < 8; ++q) {
+                pn[k][q] = 0.0f;
+                pg[k][q] = 0.0;
+            }
 #pragma unroll 1
         for (int t = 0; t < TPW; ++t) {
             const int i = 32 * (wave * TPW + t) + (lane & 31);
             float ca[8], cb[8], cc[8], f0[8], y0[8];
+            double G[8];
             load8(ws, SL_CA, i, hq, ca);
             load8(ws, SL_CB, i, hq, cb);
             load8(ws, SL_CC, i, hq, cc);
             load8(ws, SL_F0, i, hq, f0);
             load8(ws, SL_Y0, i, hq, y0);
+            if (gauss) {
 #pragma unroll
-            for (int q = 0; q < 8; ++q) {
-                const float k0 = h[q] * f0[q];
-                float v = ca[q] * th[q] + cb[q];
-                v = v * th[q] + cc[q];
-                v = v * th[q] + k0;
-                v = v * th[q] + y0[q];
-                const int env = env_base + mfma_env(q, lane);
-                if (fl[q] & 2) {
-                    const float cr = kdm_cosf(v);
-                    pn[q] = pn[q] + cr;
-                    if (gauss) {
-                        const int ge = env < p.B ? env : p.B - 1;
-#pragma unroll
-                        for (int rr = 0; rr < 4; ++rr)
-                            if (rr < p.n_rec)
-                                pg[rr][q] = pg[rr][q] + (double)cr * p.g_rec[((size_t)ge * p.n_rec + rr) * N + i];
-                    }
+                for (int q = 0; q < 8; ++q) {
+                    int env = env_base + mfma_env(q, lane);
+                    env = env < p.B ? env : p.B - 1;
+                    G[q] = p.g_rec[(size_t)env * N + i];
                 }
-                if ((fl[q] & 4) && env < p.B) p.y[(size_t)env * N + i] = v;
             }
-        }
-        (void)anyf;
-        if (__any(anyl)) {  // identical in every wave: each wave holds all 16 envs
-            rm_publish(pn);
-            if (gauss) {
 #pragma unroll
-                for (int rr = 0; rr < 4; ++rr)
-                    if (rr < p.n_rec) rm_publish_d(pg[rr], rr);
+            for (int k = 0; k < RC; ++k)
+#pragma unroll
+                for (int q = 0; q < 8; ++q) {
+                    const int f = fl[q] >> (3 * k);
+                    if (!(f & 1)) continue;
+                    const float k0 = h[q] * f0[q];
+                    const float x = th[k][q];
+                    float v = ca[q] * x + cb[q];
+                    v = v * x + cc[q];
+                    v = v * x + k0;
+                    v = v * x + y0[q];
+                    if (f & 2) {
+                        const float cr = kdm_cosf(v);
+                        pn[k][q] = pn[k][q] + cr;
+                        if (gauss) pg[k][q] = pg[k][q] + (double)cr * G[q];
+                    }
+                    const int env = env_base + mfma_env(q, lane);
+                    if ((f & 4) && env < p.B) p.y[(size_t)env * N + i] = v;
+                }
+        }
+        // identical in every wave: each wave holds all 16 envs
+        const int anyw = __any(anyl) ? (anyl | __shfl_xor(anyl, 32, 64)) : 0;
+#pragma unroll
+        for (int k = 0; k < RC; ++k) {
+            if (__any((anyl >> (3 * k)) & 2)) {
+                rm_publish(pn[k], k);
+                if (gauss) rm_publish_d(pg[k], k);
             }
         }
+        (void)anyw;
         __syncthreads();
-        if (tid < E_WG && (s_rflag[tid] & 2)) {
+        if (tid < E_WG) {
             const CtlE& c = s_ctl[tid];
-            const int si = c.si + r;
-            const float ln = rm_total(tid) / (float)N;
-            double lr = (double)ln;
-            if (gauss) {
-                double acc = 0.0;
-                for (int rr = 0; rr < p.n_rec; ++rr) acc = acc + rm_total_d(tid, rr) / (double)N;
-                lr = acc;
-            }
-            const int pos = si - c.lfp_from + c.pos0;
-            if (to_ring) {
-                p.ring[(size_t)(env_base + tid) * p.W + pos] = lr;
-            } else {
-                s_smp_n[tid][pos] = ln;
-                s_smp_r[tid][pos] = lr;
+            for (int k = 0; k < RC; ++k) {
+                if (!(s_rflag[tid][k] & 2)) continue;
+                const int si = c.si + r0 + k;
+                const float ln = rm_total(tid, k) / (float)N;
+                const double lr = gauss ? 0.0 + rm_total_d(tid, k) / (double)N : (double)ln;
+                const int pos = si - c.lfp_from + c.pos0;
+                if (to_ring) {
+                    p.ring[(size_t)(env_base + tid) * p.W + pos] = lr;
+                } else {
+                    s_smp_n[tid][pos] = ln;
+                    s_smp_r[tid][pos] = lr;
+                }
             }
         }
         __syncthreads();

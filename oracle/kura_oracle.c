@@ -288,13 +288,16 @@ static void lfp_row(const OCtx* o, Work* w, const float* row, const double* g_re
     float m = oracle_rm_f32(w->cosrow, N) / (float)N;
     *naive = m;
     if (o->cfg.rec_kernel == KURA_REC_GAUSSIAN) {
-        double acc = 0.0;
-        for (int r = 0; r < o->cfg.n_rec; ++r) {
-            const double* g = g_rec + (size_t)r * N;
-            for (int j = 0; j < N; ++j) w->prod[j] = (double)w->cosrow[j] * g[j];
-            acc = acc + oracle_rm_f64(w->prod, N) / (double)N;
+        /* sum_r mean(cos * g_r) evaluated as mean(cos * G), G = g_0 + g_1 + ...
+         * (summed in recorder order in float64).  Identical to the reference
+         * for one recorder (every shipped config); for several it differs from
+         * the per-recorder means only by float64 rounding. */
+        for (int j = 0; j < N; ++j) {
+            double G = g_rec[j];
+            for (int r = 1; r < o->cfg.n_rec; ++r) G = G + g_rec[(size_t)r * N + j];
+            w->prod[j] = (double)w->cosrow[j] * G;
         }
-        *rec = acc;
+        *rec = 0.0 + oracle_rm_f64(w->prod, N) / (double)N;
     } else {
         *rec = (double)m;
     }
