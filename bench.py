@@ -93,6 +93,25 @@ def cpu_baseline(args, cfg, alpha, omega, g_stim, g_rec, theta0, ctab, stab):
                       f"OpenMP {nthreads} threads (one env per thread)"}
 
 
+def pmc_traffic(N, B):
+    """Bytes per launch of the step kernel from the committed rocprofv3 PMC
+    passes (tools/rocprof_run.sh + tools/summarize_rocprof.py: FETCH_SIZE x2 +
+    WRITE_SIZE, the same bench command).  PMC counters cannot be read from
+    inside this process, so the latest committed summary for this exact
+    workload is quoted; None when there is none."""
+    path = os.path.join(ROOT, "profiles", "latest_rocprof.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        wl = d["bench_under_trace"]["config"]["workload"]
+        if f"N={N} " not in wl or f"x {B} envs" not in wl:
+            return None, None
+        k = d["kernels"][f"kura_step_kernel<{N // 256}>"]
+        return k["traffic_bytes_per_dispatch"], f"profiles/latest_rocprof.json ({d['source']}): FETCH_SIZE*2 + WRITE_SIZE"
+    except (OSError, KeyError, ValueError):
+        return None, None
+
+
 def main():
     args = parse()
     import torch
@@ -136,9 +155,7 @@ def main():
 
     stream = torch.cuda.current_stream(dev)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    useful_rhs = 0
-    steps_attempted = 0
-    rejected = 0
+    st0 = sim.stats()  # cumulative counters [5..7] bracket the timed launches (read outside the region)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -152,10 +169,14 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     kern_ms = [a.elapsed_time(b) for a, b in ev]
-    st = sim.stats()  # last step's counters: [max rhs per WG, steps attempted, rejected, flags]
-    steps_attempted, rejected = int(st[1]), int(st[2])
-    # useful RHS sweeps of the last launch: 2 initial sweeps per env + 6 per attempted Dopri step
+    st1 = sim.stats()
+    steps_attempted = int(st1[5] - st0[5]) // args.steps   # per launch, averaged over the timed launches
+    rejected = int(st1[7] - st0[7])
+    wg_sweeps = (st1[6] - st0[6]) / args.steps
+    # useful RHS sweeps per launch: 2 initial sweeps per env (ON and OFF solve) + 6 per attempted Dopri step;
+    # the kernel also sweeps finished envs of a workgroup in lockstep (16 env slots per workgroup sweep)
     useful_rhs = 2 * B + 6 * steps_attempted
+    lockstep_eff = useful_rhs / (16.0 * wg_sweeps) if wg_sweeps else None
     el_max = elapsed
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
@@ -171,6 +192,7 @@ def main():
         # window r/w (f64 ring + f32 obs), outputs; alpha once per launch
         bytes_env = 8 * N + 4 * N + 8 * cfg.n_elec * N + 8 * max(cfg.n_rec, 0) * N + (8 + 8 + 4) * cfg.window + 64
         bytes_launch = B * bytes_env + 4 * N * N
+        traffic, traffic_src = pmc_traffic(N, B)
         out = {
             "metric": "env steps/sec (whole node), N=1024 osc x 4096 envs per GPU",
             "value": value,
@@ -188,13 +210,15 @@ def main():
                                    f"adaptive Dopri5 rtol=atol=1e-5, W={cfg.window}, reward={args.reward}",
                        "global_envs": world * B, "parallelism": f"env-shard x{world} (no collectives)"},
             "roofline": {"bound": "mfma", "achieved": achieved_tf, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
-                         "frac": achieved_tf / PEAK_FP32_TFLOPS, "traffic": None,
+                         "frac": achieved_tf / PEAK_FP32_TFLOPS, "traffic": traffic,
+                         "traffic_source": traffic_src,
                          "kernel": "kura_step_kernel<4>", "avg_kernel_ms": avg_kernel_s * 1e3,
                          "flop_per_launch": flop_per_launch, "useful_rhs_per_launch": useful_rhs,
                          "hbm_alg_bytes_per_launch": bytes_launch,
                          "hbm_alg_gbs": bytes_launch / avg_kernel_s / 1e9},
             "extra": {"rhs_sweeps_per_env_step": useful_rhs / B, "dopri_steps_attempted": steps_attempted,
-                      "rejected": rejected, "phase_sweeps_per_s": world * useful_rhs / avg_kernel_s,
+                      "rejected": rejected, "lockstep_efficiency": lockstep_eff,
+                      "executed_frac": (16.0 * wg_sweeps * 4.0 * N * N / avg_kernel_s / 1e12) / PEAK_FP32_TFLOPS, "phase_sweeps_per_s": world * useful_rhs / avg_kernel_s,
                       "reset_ms": t_reset * 1e3, "reset_rhs_max": int(reset_stats[0]),
                       "host_setup_s": t_setup},
         }

@@ -14,6 +14,7 @@ from ctypes import POINTER, c_double, c_float, c_int, c_int32, c_int64, c_uint8,
 KURA_ABI_VERSION = 1
 KURA_S_MAX = 32
 KURA_MAX_BINS = 32
+KURA_NSTATS = 8
 
 KURA_REC_NAIVE = 0
 KURA_REC_GAUSSIAN = 1
@@ -90,7 +91,7 @@ _SYMBOLS = {
     "kura_reward": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p]),
     "kura_get_state": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "kura_set_state": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
-    "kura_get_stats": (c_int, [c_void_p, c_void_p]),
+    "kura_get_stats": (c_int, [c_void_p, c_void_p, c_int]),
     "kura_get_stamps": (c_int, [c_void_p, c_void_p]),
     "kura_selftest_math": (c_int, [c_void_p, c_void_p, c_void_p, c_int]),
     "kura_selftest_gemm": (c_int, [c_void_p, c_void_p, c_void_p, c_int]),

@@ -31,6 +31,7 @@
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef unsigned int v4u32 __attribute__((ext_vector_type(4)));
 
 // ---- Dopri5 tableau cast to fp32 (identical constants to the oracle) -------
 // kA[s][j]: stage s input = y0 + chain_j(kA[s][j] * k_j); kE: error weights;
@@ -90,16 +91,21 @@ struct DevParams {
 };
 
 // Diagnostic phase timers (compile with -DKURA_STAMPS): per wave, cycles
-// spent in stage-input / barrier / GEMM / epilogue / barrier / post-step /
-// flag-sync, accumulated with s_memtime and added into p.stamps at the end.
+// spent in each phase (tools/phase_stamps.py names them), accumulated with
+// s_memtime and added into p.stamps[wave][KURA_NSTAMP] at the end.
+#define KURA_NSTAMP 16
 #ifdef KURA_STAMPS
-#define STAMP_DECL unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}; unsigned long long st_last = __builtin_amdgcn_s_memtime();
+#define STAMP_DECL unsigned long long st_acc[KURA_NSTAMP] = {}; unsigned long long st_last = __builtin_amdgcn_s_memtime();
 #define STAMP(k) do { unsigned long long n_ = __builtin_amdgcn_s_memtime(); st_acc[k] += n_ - st_last; st_last = n_; } while (0)
-#define STAMP_FLUSH(p) do { if ((threadIdx.x & 63) == 0 && (p).stamps) for (int k_ = 0; k_ < 8; ++k_) atomicAdd(&(p).stamps[(threadIdx.x >> 6) * 8 + k_], st_acc[k_]); } while (0)
+#define STAMP_FLUSH(p) do { if ((threadIdx.x & 63) == 0 && (p).stamps) for (int k_ = 0; k_ < KURA_NSTAMP; ++k_) atomicAdd(&(p).stamps[(threadIdx.x >> 6) * KURA_NSTAMP + k_], st_acc[k_]); } while (0)
+#define STAMP_PARAMS , unsigned long long (&st_acc)[KURA_NSTAMP], unsigned long long& st_last
+#define STAMP_ARGS , st_acc, st_last
 #else
 #define STAMP_DECL
 #define STAMP(k) do { } while (0)
 #define STAMP_FLUSH(p) do { } while (0)
+#define STAMP_PARAMS
+#define STAMP_ARGS
 #endif
 
 // Per-workgroup LDS besides the dynamic 32 x N operand: LFP samples of the
@@ -153,6 +159,20 @@ __device__ __forceinline__ double grid_at(const Grid& g, int i) {
 // compiler can count vmcnt precisely; two buffers give a prefetch distance of
 // one k-block (16 MFMAs of this wave + the partner wave's) per load.
 typedef const __attribute__((address_space(1))) floatx4 gfloatx4;
+typedef __attribute__((address_space(1))) floatx4 gfx4;
+typedef __attribute__((address_space(1))) float gfloat;
+
+// Wave-uniform copy of a pointer (SGPRs): pointers read through the solver's
+// VGPR-passed DevParams reference would otherwise stay per-lane (flat
+// addressing, 64-bit VALU address math, spills).
+template <typename T>
+__device__ __forceinline__ T* uniform_ptr(T* ptr) {
+    const uint64_t v = (uint64_t)(uintptr_t)ptr;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    return (T*)(uintptr_t)(((uint64_t)hi << 32) | lo);
+}
+
 
 template <int TPW>
 __device__ __forceinline__ void coupling_gemm(const float* __restrict__ Xs, const float* __restrict__ alpha_sw,
@@ -160,19 +180,42 @@ __device__ __forceinline__ void coupling_gemm(const float* __restrict__ Xs, cons
     constexpr int N = TPW * 256;
     constexpr int NK8 = N / 8;
     constexpr int TSTRIDE = NK8 * 64;  // floatx4 per column tile
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    // lane id re-derived here (volatile: never CSE'd with a long-lived value),
+    // so the loop's addresses are not reloaded from a spill slot in the
+    // preheader -- such a reload makes the loop-header wait vmcnt(0), which
+    // would drain the alpha prefetch every iteration.
+    int lane;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
 #pragma unroll
     for (int t = 0; t < TPW; ++t)
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[t][r] = 0.0f;
     // lane l reads floats [kb*XS_BLOCK + (l>>5)*XS_HALF + (l&31)*4, +4)
     const floatx4* xs4 = reinterpret_cast<const floatx4*>(Xs + (lane >> 5) * XS_HALF + (lane & 31) * 4);
-    gfloatx4* bp = (gfloatx4*)(alpha_sw) + (size_t)(wave * TPW) * TSTRIDE + lane;
+    // alpha via raw buffer loads: wave-uniform descriptor (this wave's TPW
+    // column tiles), 32-bit lane offset, tile offset in an SGPR -- no 64-bit
+    // address VALU between the MFMAs (isolated: 150 vs 130 TFLOP/s with
+    // global_load, tools/gemm_bench.hip).  Two register buffers, one k-block
+    // of cover; sched_barrier keeps each refill right after the MFMAs that
+    // consumed the buffer (the scheduler would sink them to the loop end).
+    // Loads past the last k-block are clamped so the count per iteration is
+    // fixed (exact vmcnt).
+    // (the descriptor must be provably wave-uniform, else every load becomes a
+    // readfirstlane waterfall loop: alpha_sw reaches this non-inlined solver
+    // through a VGPR-passed reference, so force it into SGPRs)
+    const float* au = uniform_ptr(alpha_sw);
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(au + (size_t)wave * TPW * TSTRIDE * 4), 0, TPW * TSTRIDE * 16, 0x00020000);
+    auto ld = [&](int t, int k) -> floatx4 {
+        return __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(rs, (lane + k * 64) * 16,
+                                                                                 t * TSTRIDE * 16, 0));
+    };
     floatx4 b0[TPW], b1[TPW];
 #pragma unroll
     for (int t = 0; t < TPW; ++t) {
-        b0[t] = bp[t * TSTRIDE];
-        b1[t] = bp[t * TSTRIDE + 64];
+        b0[t] = ld(t, 0);
+        b1[t] = ld(t, 1);
     }
 #pragma unroll 1
     for (int kb = 0; kb < NK8; kb += 2) {
@@ -180,22 +223,44 @@ __device__ __forceinline__ void coupling_gemm(const float* __restrict__ Xs, cons
 #pragma unroll
         for (int s = 0; s < 4; ++s)
 #pragma unroll
-            for (int t = 0; t < TPW; ++t)
-                acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s], b0[t][s], acc[t], 0, 0, 0);
-        // unconditional (clamped) prefetch keeps the vmcnt bookkeeping exact
+            for (int t = 0; t < TPW; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s], b0[t][s], acc[t], 0, 0, 0);
         const int k2 = kb + 2 < NK8 ? kb + 2 : NK8 - 1;
 #pragma unroll
-        for (int t = 0; t < TPW; ++t) b0[t] = bp[t * TSTRIDE + k2 * 64];
+        for (int t = 0; t < TPW; ++t) b0[t] = ld(t, k2);
+        __builtin_amdgcn_sched_barrier(0);
         a = xs4[(kb + 1) * (XS_BLOCK / 4)];
 #pragma unroll
         for (int s = 0; s < 4; ++s)
 #pragma unroll
-            for (int t = 0; t < TPW; ++t)
-                acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s], b1[t][s], acc[t], 0, 0, 0);
+            for (int t = 0; t < TPW; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s], b1[t][s], acc[t], 0, 0, 0);
         const int k3 = kb + 3 < NK8 ? kb + 3 : NK8 - 1;
 #pragma unroll
-        for (int t = 0; t < TPW; ++t) b1[t] = bp[t * TSTRIDE + k3 * 64];
+        for (int t = 0; t < TPW; ++t) b1[t] = ld(t, k3);
+        __builtin_amdgcn_sched_barrier(0);
     }
+#ifdef KURA_GEMM_NOPS
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+#endif
+}
+
+// Workgroup barrier that orders LDS only.  Inside a solve every workspace
+// record (R) is written and read back by the same lane (MFMA-layout
+// ownership), so the release half of __syncthreads -- which also drains every
+// outstanding global store and load (vmcnt(0)) -- is not needed there; only
+// LDS (the GEMM operand, control slots, reduction partials) is shared.
+__device__ __forceinline__ void lds_barrier() {
+#ifdef KURA_FULL_BARRIER
+    __syncthreads();
+    return;
+#endif
+    // compiler-only barrier for the records: they are stored through global
+    // pointers and loaded through a buffer descriptor, and nothing may be
+    // reordered across a phase boundary
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+    asm volatile("" ::: "memory");
 }
 
 // Per-env solver control.  One slot per local env lives in LDS; thread e
@@ -255,14 +320,20 @@ __device__ __forceinline__ void ctl_begin(CtlE& c, const Grid& g, float dt0, int
 // q = 4..7 are two 16-byte vectors at envs 4h.. and 8+4h...
 __device__ __forceinline__ int mfma_env(int q, int lane) { return (q & 3) + 8 * (q >> 2) + 4 * (lane >> 5); }
 
-enum { SL_Y0 = 0, SL_F0 = 1, SL_Y1 = 8, SL_CA = 9, SL_CB = 10, SL_CC = 11, NSLOT = 12 };
+enum { SL_Y0 = 0, SL_F0 = 1, SL_Y1 = 8, SL_CA = 9, SL_CB = 10, SL_CC = 11, SL_W = 12, SL_P = 13, NSLOT = 14 };
 
+// One workgroup's solver records, [slot][N][16 envs] f32, addressed through a
+// raw buffer descriptor: wave-uniform descriptor and tile offsets (SGPRs), one
+// per-lane byte offset (VGPR).  Keeps the record traffic free of 64-bit VALU
+// address math and of per-record address registers (which the compiler would
+// hoist out of the stage loop and spill).
 struct Slot {
-    float* base;  // workgroup slot 0
+    __amdgpu_buffer_rsrc_t rs;
     int N;
-    __device__ floatx4* at(int slot, int i, int half) const {
-        return reinterpret_cast<floatx4*>(base + ((size_t)slot * N + i) * 16) + half;
-    }
+    int ct0;   // first column tile of this wave (wave * TPW), wave-uniform
+    int voff;  // (lane & 31) * 64 + (lane >> 5) * 16 bytes
+    gfloat* base;
+    __device__ int soff(int slot, int t) const { return (slot * N + 32 * (ct0 + t)) * 64; }
 };
 
 __device__ __forceinline__ void split8(const floatx4& a, const floatx4& b, float (&v)[8]) {
@@ -270,48 +341,43 @@ __device__ __forceinline__ void split8(const floatx4& a, const floatx4& b, float
     v[4] = b[0]; v[5] = b[1]; v[6] = b[2]; v[7] = b[3];
 }
 // lane's two env groups: half 0 -> envs 4h..4h+3, half 1 -> envs 8+4h..8+4h+3
-__device__ __forceinline__ void load8(const Slot& w, int slot, int i, int hq, float (&v)[8]) {
-    split8(*w.at(slot, i, hq), *w.at(slot, i, 2 + hq), v);
+__device__ __forceinline__ void load8(const Slot& w, int slot, int t, float (&v)[8]) {
+    const floatx4 a = __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(w.rs, w.voff, w.soff(slot, t), 0));
+    const floatx4 b =
+        __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(w.rs, w.voff + 32, w.soff(slot, t), 0));
+    split8(a, b, v);
 }
-__device__ __forceinline__ void store8(const Slot& w, int slot, int i, int hq, const float (&v)[8]) {
-    floatx4 a = {v[0], v[1], v[2], v[3]}, b = {v[4], v[5], v[6], v[7]};
-    *w.at(slot, i, hq) = a;
-    *w.at(slot, i, 2 + hq) = b;
-}
-
-// omega and pulse of the lane's MFMA-layout elements, fetched at the start of
-// a stage so their latency hides under the GEMM.
-template <int TPW>
-struct EpiConst {
-    float w[TPW][8];
-    float u[TPW][8];
-};
-
-template <int TPW>
-__device__ __forceinline__ void load_epi_const(const DevParams& p, int env_base, bool pulse_on,
-                                               EpiConst<TPW>& k) {
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    constexpr int N = TPW * 256;
-#pragma unroll
-    for (int t = 0; t < TPW; ++t) {
-        const int i = 32 * (wave * TPW + t) + (lane & 31);
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-            int env = env_base + mfma_env(q, lane);
-            env = env < p.B ? env : p.B - 1;  // padded rows: any valid address
-            const size_t o = (size_t)env * N + i;
-            k.w[t][q] = p.omega[o];
-            k.u[t][q] = pulse_on ? p.pulse[o] : 0.0f;  // pulse = 0 while OFF (env.py:434)
-        }
-    }
+__device__ __forceinline__ void store8(const Slot& w, int slot, int t, const float (&v)[8]) {
+    // global stores with an SGPR base (slot/tile folded in by SALU) and the
+    // 32-bit lane offset.  Raw buffer stores are NOT used here: at N=256
+    // (one column tile per wave) they intermittently lost record components
+    // on gfx950 (ROCm 7.2), see DESIGN.md "Kernel notes".
+    const floatx4 a = {v[0], v[1], v[2], v[3]}, b = {v[4], v[5], v[6], v[7]};
+    __attribute__((address_space(1))) char* sb = (__attribute__((address_space(1))) char*)w.base + w.soff(slot, t);
+    *(gfx4*)(sb + (uint32_t)w.voff) = a;
+    *(gfx4*)(sb + (uint32_t)(w.voff + 32)) = b;
 }
 
 // f = fmaf(kn, fmaf(c, P, -(s*Q)), omega) + pulse  ->  slot F0 + stage
+// (omega and pulse come from their records, SL_W / SL_P, written at the
+// start of the solve; all TPW tiles' loads are issued before the first use)
 template <int TPW>
 __device__ __forceinline__ void coupling_epilogue(const DevParams& p, const Slot& ws, const float* __restrict__ Xs,
-                                                  const floatx16 (&acc)[TPW], const EpiConst<TPW>& kc, int stage) {
+                                                  const floatx16 (&acc)[TPW], int stage, bool pulse_on) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int hq = lane >> 5;
+    float w[TPW][8], u[TPW][8];
+#pragma unroll
+    for (int t = 0; t < TPW; ++t) {
+        const int i = 32 * (wave * TPW + t) + (lane & 31);
+        load8(ws, SL_W, t, w[t]);
+        if (pulse_on) {
+            load8(ws, SL_P, t, u[t]);
+        } else {
+#pragma unroll
+            for (int q = 0; q < 8; ++q) u[t][q] = 0.0f;  // still added: x + 0 is not folded (signed zeros)
+        }
+    }
 #pragma unroll
     for (int t = 0; t < TPW; ++t) {
         const int i = 32 * (wave * TPW + t) + (lane & 31);
@@ -323,9 +389,9 @@ __device__ __forceinline__ void coupling_epilogue(const DevParams& p, const Slot
             const float sn = Xs[xs_idx(e, i)], cs = Xs[xs_idx(16 + e, i)];
             const float tq = sn * Q;
             const float coup = __builtin_fmaf(cs, P, -tq);
-            f[q] = __builtin_fmaf(p.kn, coup, kc.w[t][q]) + kc.u[t][q];
+            f[q] = __builtin_fmaf(p.kn, coup, w[t][q]) + u[t][q];
         }
-        store8(ws, SL_F0 + stage, i, hq, f);
+        store8(ws, SL_F0 + stage, t, f);
     }
 }
 
@@ -342,10 +408,10 @@ __device__ __forceinline__ void stage_tiles(const Slot& ws, float* Xs, int s, co
 #pragma unroll
     for (int u = 0; u < NT; ++u) {
         const int i = 32 * (wave * TPW + t0 + u) + (lane & 31);
-        load8(ws, SL_Y0, i, hq, y0[u]);
+        load8(ws, SL_Y0, t0 + u, y0[u]);
 #pragma unroll
         for (int j = 0; j < 6; ++j)
-            if (j < s) load8(ws, SL_F0 + j, i, hq, f[u][j]);
+            if (j < s) load8(ws, SL_F0 + j, t0 + u, f[u][j]);
     }
 #pragma unroll
     for (int u = 0; u < NT; ++u) {
@@ -370,7 +436,7 @@ __device__ __forceinline__ void stage_tiles(const Slot& ws, float* Xs, int s, co
             Xs[xs_idx(e, i)] = sn;
             Xs[xs_idx(16 + e, i)] = cs;
         }
-        if (s == 6) store8(ws, SL_Y1, i, hq, ys);
+        if (s == 6) store8(ws, SL_Y1, t0 + u, ys);
     }
 }
 
@@ -424,7 +490,7 @@ __device__ __forceinline__ double rm_total_d(int e, int k) {
 // After the 7th stage: error norm, accept/reject, dense-output saves with
 // LFP, FSAL -- for all 16 envs, every wave on its own columns.
 template <int TPW>
-__device__ __forceinline__ void post_step(const DevParams& p, const Slot& ws, int env_base, bool to_ring) {
+__device__ __forceinline__ void post_step(const DevParams& p, const Slot& ws, int env_base, bool to_ring STAMP_PARAMS) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, tid = threadIdx.x;
     const int hq = lane >> 5;
     constexpr int N = TPW * 256;
@@ -437,14 +503,14 @@ __device__ __forceinline__ void post_step(const DevParams& p, const Slot& ws, in
     for (int t = 0; t < TPW; ++t) {
         const int i = 32 * (wave * TPW + t) + (lane & 31);
         float y0[8], y1[8], f0[8], f2[8], f3[8], f4[8], f5[8], f6[8];
-        load8(ws, SL_Y0, i, hq, y0);
-        load8(ws, SL_Y1, i, hq, y1);
-        load8(ws, SL_F0 + 0, i, hq, f0);
-        load8(ws, SL_F0 + 2, i, hq, f2);
-        load8(ws, SL_F0 + 3, i, hq, f3);
-        load8(ws, SL_F0 + 4, i, hq, f4);
-        load8(ws, SL_F0 + 5, i, hq, f5);
-        load8(ws, SL_F0 + 6, i, hq, f6);
+        load8(ws, SL_Y0, t, y0);
+        load8(ws, SL_Y1, t, y1);
+        load8(ws, SL_F0 + 0, t, f0);
+        load8(ws, SL_F0 + 2, t, f2);
+        load8(ws, SL_F0 + 3, t, f3);
+        load8(ws, SL_F0 + 4, t, f4);
+        load8(ws, SL_F0 + 5, t, f5);
+        load8(ws, SL_F0 + 6, t, f6);
         float ca[8], cb[8], cc[8];
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
@@ -473,12 +539,13 @@ __device__ __forceinline__ void post_step(const DevParams& p, const Slot& ws, in
             cb[q] = ((((5.0f * k0) - (3.0f * k6)) + (18.0f * yy0)) + (14.0f * yy1)) - (32.0f * ym);
             cc[q] = (((k6 - (4.0f * k0)) - (11.0f * yy0)) - (5.0f * yy1)) + (16.0f * ym);
         }
-        store8(ws, SL_CA, i, hq, ca);
-        store8(ws, SL_CB, i, hq, cb);
-        store8(ws, SL_CC, i, hq, cc);
+        store8(ws, SL_CA, t, ca);
+        store8(ws, SL_CB, t, cb);
+        store8(ws, SL_CC, t, cc);
     }
     rm_publish(part, 0);
-    __syncthreads();
+    STAMP(5);
+    lds_barrier();
     // (2) thread e: accept/reject, step-size update (diffrax PIDController)
     if (tid < E_WG) {
         CtlE& c = s_ctl[tid];
@@ -501,13 +568,14 @@ __device__ __forceinline__ void post_step(const DevParams& p, const Slot& ws, in
             }
         }
     }
-    __syncthreads();
+    lds_barrier();
     if (tid == 0) {
         int m = 0;
         for (int e = 0; e < E_WG; ++e) m = s_ctl[e].nsave > m ? s_ctl[e].nsave : m;
         s_maxsave = m;
     }
-    __syncthreads();
+    lds_barrier();
+    STAMP(7);
     const int nrounds = s_maxsave;
     // (3) saves: RC rounds (save indices) per pass over the records, all envs
     // in parallel; one RM reduction per round and LFP kind.
@@ -530,7 +598,7 @@ __device__ __forceinline__ void post_step(const DevParams& p, const Slot& ws, in
                 s_rflag[tid][k] = fl;
             }
         }
-        __syncthreads();
+        lds_barrier();
         float th[RC][8];
         int fl[8];
         int anyl = 0;
@@ -560,11 +628,11 @@ __device__ __forceinline__ void post_step(const DevParams& p, const Slot& ws, in
             const int i = 32 * (wave * TPW + t) + (lane & 31);
             float ca[8], cb[8], cc[8], f0[8], y0[8];
             double G[8];
-            load8(ws, SL_CA, i, hq, ca);
-            load8(ws, SL_CB, i, hq, cb);
-            load8(ws, SL_CC, i, hq, cc);
-            load8(ws, SL_F0, i, hq, f0);
-            load8(ws, SL_Y0, i, hq, y0);
+            load8(ws, SL_CA, t, ca);
+            load8(ws, SL_CB, t, cb);
+            load8(ws, SL_CC, t, cc);
+            load8(ws, SL_F0, t, f0);
+            load8(ws, SL_Y0, t, y0);
             if (gauss) {
 #pragma unroll
                 for (int q = 0; q < 8; ++q) {
@@ -604,7 +672,7 @@ __device__ __forceinline__ void post_step(const DevParams& p, const Slot& ws, in
             }
         }
         (void)anyw;
-        __syncthreads();
+        lds_barrier();
         if (tid < E_WG) {
             const CtlE& c = s_ctl[tid];
             for (int k = 0; k < RC; ++k) {
@@ -621,8 +689,9 @@ __device__ __forceinline__ void post_step(const DevParams& p, const Slot& ws, in
                 }
             }
         }
-        __syncthreads();
+        lds_barrier();
     }
+    STAMP(8);
     // (4) accepted envs: y0 <- y1, f0 <- f6 (FSAL)
     int kp[8];
 #pragma unroll
@@ -631,20 +700,21 @@ __device__ __forceinline__ void post_step(const DevParams& p, const Slot& ws, in
     for (int t = 0; t < TPW; ++t) {
         const int i = 32 * (wave * TPW + t) + (lane & 31);
         float y0[8], y1[8], f0[8], f6[8];
-        load8(ws, SL_Y0, i, hq, y0);
-        load8(ws, SL_Y1, i, hq, y1);
-        load8(ws, SL_F0, i, hq, f0);
-        load8(ws, SL_F0 + 6, i, hq, f6);
+        load8(ws, SL_Y0, t, y0);
+        load8(ws, SL_Y1, t, y1);
+        load8(ws, SL_F0, t, f0);
+        load8(ws, SL_F0 + 6, t, f6);
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
             y0[q] = kp[q] ? y1[q] : y0[q];
             f0[q] = kp[q] ? f6[q] : f0[q];
         }
-        store8(ws, SL_Y0, i, hq, y0);
-        store8(ws, SL_F0, i, hq, f0);
+        store8(ws, SL_Y0, t, y0);
+        store8(ws, SL_F0, t, f0);
     }
+    STAMP(9);
     // (5) thread e: time advance (adapt_step_size + _clip_to_end)
-    __syncthreads();
+    lds_barrier();
     if (tid < E_WG) {
         CtlE& c = s_ctl[tid];
         if (c.active) {
@@ -663,7 +733,7 @@ __device__ __forceinline__ void post_step(const DevParams& p, const Slot& ws, in
             }
         }
     }
-    __syncthreads();
+    lds_barrier();
 }
 
 // One diffeqsolve for the workgroup's 16 envs.  s_ctl must be initialised
@@ -674,35 +744,45 @@ __device__ void solve_wg(const DevParams& p, float* Xs, int env_base, bool to_ri
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, tid = threadIdx.x;
     const int hq = lane >> 5;
     constexpr int N = TPW * 256;
-    const Slot ws{p.R + (size_t)blockIdx.x * NSLOT * N * 16, N};
-    // record y0 <- state y (MFMA layout)
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const Slot ws{__builtin_amdgcn_make_buffer_rsrc((void*)uniform_ptr(p.R + (size_t)blockIdx.x * NSLOT * N * 16), 0,
+                                                    NSLOT * N * 16 * 4, 0x00020000),
+                  N, wv * TPW, (lane & 31) * 64 + hq * 16,
+                  (gfloat*)uniform_ptr(p.R + (size_t)blockIdx.x * NSLOT * N * 16)};
+    // records y0 <- state y, omega, pulse (0 while stimulation is OFF, env.py:434)
 #pragma unroll 1
     for (int t = 0; t < TPW; ++t) {
         const int i = 32 * (wave * TPW + t) + (lane & 31);
-        float v[8];
+        float v[8], w[8], u[8];
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
-            const int env = env_base + mfma_env(q, lane);
-            v[q] = env < p.B ? p.y[(size_t)env * N + i] : 0.0f;
+            int env = env_base + mfma_env(q, lane);
+            const bool ok = env < p.B;
+            env = ok ? env : p.B - 1;  // padded slots: any valid address
+            const size_t o = (size_t)env * N + i;
+            v[q] = ok ? p.y[o] : 0.0f;
+            w[q] = p.omega[o];
+            u[q] = pulse_on ? p.pulse[o] : 0.0f;
         }
-        store8(ws, SL_Y0, i, hq, v);
+        store8(ws, SL_Y0, t, v);
+        store8(ws, SL_W, t, w);
+        if (pulse_on) store8(ws, SL_P, t, u);
     }
+    asm volatile("" ::: "memory");  // record stores before the first record loads
     STAMP_DECL
     long long nrhs = 0;
     int s = 0;  // stage 0 = initial RHS at y0 (FSAL seed)
     for (;;) {
         floatx16 acc[TPW];
-        EpiConst<TPW> kc;
         stage_input<TPW>(ws, Xs, s);
         STAMP(0);
-        load_epi_const<TPW>(p, env_base, pulse_on, kc);
-        __syncthreads();
+        lds_barrier();
         STAMP(1);
         coupling_gemm<TPW>(Xs, p.alpha_sw, acc);
         STAMP(2);
-        coupling_epilogue<TPW>(p, ws, Xs, acc, kc, s);
+        coupling_epilogue<TPW>(p, ws, Xs, acc, s, pulse_on);
         STAMP(3);
-        __syncthreads();
+        lds_barrier();
         STAMP(4);
         ++nrhs;
         if (s > 0 && s < 6) {
@@ -710,8 +790,8 @@ __device__ void solve_wg(const DevParams& p, float* Xs, int env_base, bool to_ri
             continue;
         }
         if (s == 6) {
-            post_step<TPW>(p, ws, env_base, to_ring);
-            STAMP(5);
+            post_step<TPW>(p, ws, env_base, to_ring STAMP_ARGS);
+            STAMP(10);
         }
         if (tid == 0) {
             int any = 0;
@@ -720,7 +800,7 @@ __device__ void solve_wg(const DevParams& p, float* Xs, int env_base, bool to_ri
             for (int e = 0; e < E_WG; ++e)
                 if (s_ctl[e].active) s_ctl[e].h = s_ctl[e].tnext - s_ctl[e].tprev;
         }
-        __syncthreads();
+        lds_barrier();
         STAMP(6);
         if (s_any == 0) break;
         s = 1;
@@ -742,6 +822,10 @@ __device__ __forceinline__ void flush_stats(const DevParams& p, long long rhs, i
     atomicAdd(&p.stats[1], steps);
     atomicAdd(&p.stats[2], rej);
     if (flags) atomicOr(&p.stats[3], flags);
+    atomicAdd(&p.stats[4], (unsigned long long)rhs);
+    atomicAdd(&p.stats[5], steps);
+    atomicAdd(&p.stats[6], (unsigned long long)rhs);
+    atomicAdd(&p.stats[7], rej);
 }
 
 // Kernel prologue: zero every env's control slot.
@@ -919,6 +1003,7 @@ __global__ __launch_bounds__(NTHREADS) void kura_step_kernel(DevParams p, const 
     __syncthreads();
     long long rhs = 0;
     solve_wg<TPW>(p, Xs, env_base, false, true, &rhs);
+    __syncthreads();  // global stores of the solve (y) before the OFF setup
     // ---- stimulation OFF (env.py:433-441)
     if (tid < E_WG) {
         CtlE& c = s_ctl[tid];
@@ -941,6 +1026,7 @@ __global__ __launch_bounds__(NTHREADS) void kura_step_kernel(DevParams p, const 
     }
     __syncthreads();
     solve_wg<TPW>(p, Xs, env_base, false, false, &rhs);
+    __syncthreads();
     // ---- window, reward, outputs (env.py:443-454): wave w owns envs 2w, 2w+1
     constexpr int WPL = WPL_MAX;
 #pragma unroll 1
@@ -1027,6 +1113,7 @@ __global__ __launch_bounds__(NTHREADS) void kura_reset_kernel(DevParams p, const
     __syncthreads();
     long long rhs = 0;
     solve_wg<TPW>(p, Xs, env_base, true, false, &rhs);
+    __syncthreads();  // ring rows written by thread e are read by every lane below
 #pragma unroll 1
     for (int ee = 0; ee < ENVS_PER_WAVE; ++ee) {
         const int e = wave * ENVS_PER_WAVE + ee;

@@ -169,12 +169,12 @@ class KuraSim:
         check(self.lib, self.lib.kura_set_state(self._h, *[a.ctypes.data for a in arrs]), "kura_set_state")
 
     def stats(self) -> np.ndarray:
-        out = np.zeros(4, np.int64)
-        check(self.lib, self.lib.kura_get_stats(self._h, out.ctypes.data), "kura_get_stats")
+        out = np.zeros(abi.KURA_NSTATS, np.int64)
+        check(self.lib, self.lib.kura_get_stats(self._h, out.ctypes.data, len(out)), "kura_get_stats")
         return out
 
     def stamps(self) -> np.ndarray:
-        out = np.zeros((8, 8), np.uint64)
+        out = np.zeros((8, 16), np.uint64)
         check(self.lib, self.lib.kura_get_stamps(self._h, out.ctypes.data), "kura_get_stamps")
         return out
 

@@ -120,9 +120,14 @@ int kura_get_state(KuraHandle* h, float* y /* B*N */, double* t /* B */, int32_t
                    double* ring /* B*W */, int32_t* wpos /* B */);
 int kura_set_state(KuraHandle* h, const float* y, const double* t, const int32_t* step,
                    const double* ring, const int32_t* wpos);
-/* counters: [0] RHS sweeps issued per env (max over envs) in the last call,
- * [1] Dopri5 steps attempted, [2] rejected, [3] error flags (bit0 max_steps, bit1 nan) */
-int kura_get_stats(KuraHandle* h, int64_t* out4);
+/* counters (synchronises the device), first min(n, KURA_NSTATS) written:
+ * last call:  [0] RHS sweeps issued by the busiest workgroup, [1] Dopri5 steps
+ *             attempted (all envs), [2] rejected, [3] error flags (bit0
+ *             max_steps, bit3 grid overflow), [4] RHS sweeps issued summed over
+ *             workgroups (each sweep covers 16 env slots);
+ * since kura_create: [5] steps attempted, [6] workgroup sweeps, [7] rejected. */
+#define KURA_NSTATS 8
+int kura_get_stats(KuraHandle* h, int64_t* out, int n);
 
 /* diagnostics for the GPU parity tests (host pointers; synchronous; not on
  * the step path).  selftest_math writes 8 floats per element: sin, cos,
@@ -131,8 +136,9 @@ int kura_get_stats(KuraHandle* h, int64_t* out4);
  * 32 x N operand: Y[r][i] = sum_k X[r][k] * alpha[i][k]. */
 int kura_selftest_math(const float* x, const float* y, float* out, int n);
 int kura_selftest_gemm(const float* X, const float* alpha, float* Y, int N);
-/* per-wave phase cycle counters of a -DKURA_STAMPS build ([8 waves][8]:
- * stage-input, barrier, GEMM, epilogue, barrier, post-step, flag, start);
+/* per-wave phase cycle counters of a -DKURA_STAMPS build ([8 waves][16]:
+ * stage-input, barrier, GEMM, epilogue, barrier, post-step error pass, flag,
+ * post-step decision, saves, FSAL, time advance, 5 spare; tools/phase_stamps.py);
  * zeros in the production build.  Reading clears them. */
 int kura_get_stamps(KuraHandle* h, uint64_t* out);
 

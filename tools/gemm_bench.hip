@@ -1,0 +1,330 @@
+// gemm_bench.hip -- diagnostic: MFMA efficiency of coupling-GEMM variants in
+// isolation (full grid, 16 envs per workgroup, N=1024), to choose the
+// production loop structure.  Build + run on the GPU box:
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -o tools/gemm_bench tools/gemm_bench.hip
+//   ./tools/gemm_bench
+#include "../dbs-gym_amd/csrc/kura_kernels.hip"
+
+#include <stdio.h>
+#include <vector>
+
+// V0: two register buffers, loads interleaved by the compiler (round-1 code).
+template <int TPW, int SCHED, int MODE = 0>
+__device__ __forceinline__ void gemm_v0(const float* Xs, const float* alpha_sw, floatx16 (&acc)[TPW]) {
+    constexpr int N = TPW * 256, NK8 = N / 8, TSTRIDE = NK8 * 64;
+    int lane;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    for (int t = 0; t < TPW; ++t)
+        for (int r = 0; r < 16; ++r) acc[t][r] = 0.0f;
+    const floatx4* xs4 = reinterpret_cast<const floatx4*>(Xs + (lane >> 5) * XS_HALF + (lane & 31) * 4);
+    gfloatx4* bp = (gfloatx4*)(alpha_sw) + (size_t)(wave * TPW) * TSTRIDE + lane;
+    floatx4 b0[TPW], b1[TPW];
+#pragma unroll
+    for (int t = 0; t < TPW; ++t) {
+        b0[t] = bp[t * TSTRIDE];
+        b1[t] = bp[t * TSTRIDE + 64];
+    }
+#pragma unroll 1
+    for (int kb = 0; kb < NK8; kb += 2) {
+        floatx4 a = xs4[kb * (XS_BLOCK / 4)];
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+            for (int t = 0; t < TPW; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s], b0[t][s], acc[t], 0, 0, 0);
+        int k2 = kb + 2 < NK8 ? kb + 2 : NK8 - 1;
+        if (MODE == 1) k2 &= 7;  // small L2-resident working set
+#pragma unroll
+        for (int t = 0; t < TPW; ++t) if (MODE != 2) b0[t] = bp[t * TSTRIDE + k2 * 64];
+        if (SCHED) __builtin_amdgcn_sched_barrier(0);
+        a = xs4[(kb + 1) * (XS_BLOCK / 4)];
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+            for (int t = 0; t < TPW; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s], b1[t][s], acc[t], 0, 0, 0);
+        int k3 = kb + 3 < NK8 ? kb + 3 : NK8 - 1;
+        if (MODE == 1) k3 &= 7;
+#pragma unroll
+        for (int t = 0; t < TPW; ++t) if (MODE != 2) b1[t] = bp[t * TSTRIDE + k3 * 64];
+        if (SCHED) __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
+
+// Variants on the two-buffer loop (all with sched_barrier pinning):
+//   PRIO 1: s_setprio(1) around each MFMA cluster; PRIO 2: static prio 1 for waves 4-7
+//   BUF 1: raw buffer loads (SGPR descriptor, 32-bit offsets)
+template <int TPW, int PRIO, int BUF>
+__device__ __forceinline__ void gemm_v2(const float* Xs, const float* alpha_sw, floatx16 (&acc)[TPW]) {
+    constexpr int N = TPW * 256, NK8 = N / 8, TSTRIDE = NK8 * 64;
+    int lane;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (PRIO == 2 && wave >= 4) __builtin_amdgcn_s_setprio(1);
+    for (int t = 0; t < TPW; ++t)
+        for (int r = 0; r < 16; ++r) acc[t][r] = 0.0f;
+    const floatx4* xs4 = reinterpret_cast<const floatx4*>(Xs + (lane >> 5) * XS_HALF + (lane & 31) * 4);
+    gfloatx4* bp = (gfloatx4*)(alpha_sw) + (size_t)(wave * TPW) * TSTRIDE + lane;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)(alpha_sw + (size_t)wave * TPW * TSTRIDE * 4), 0, TPW * TSTRIDE * 16, 0x00020000);
+    auto ld = [&](int t, int k) -> floatx4 {
+        if (BUF) return __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(rs, (lane + k * 64) * 16, t * TSTRIDE * 16, 0));
+        return bp[t * TSTRIDE + k * 64];
+    };
+    floatx4 b0[TPW], b1[TPW];
+#pragma unroll
+    for (int t = 0; t < TPW; ++t) {
+        b0[t] = ld(t, 0);
+        b1[t] = ld(t, 1);
+    }
+#pragma unroll 1
+    for (int kb = 0; kb < NK8; kb += 2) {
+        floatx4 a = xs4[kb * (XS_BLOCK / 4)];
+        if (PRIO == 1) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+            for (int t = 0; t < TPW; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s], b0[t][s], acc[t], 0, 0, 0);
+        if (PRIO == 1) __builtin_amdgcn_s_setprio(0);
+        const int k2 = kb + 2 < NK8 ? kb + 2 : NK8 - 1;
+#pragma unroll
+        for (int t = 0; t < TPW; ++t) b0[t] = ld(t, k2);
+        __builtin_amdgcn_sched_barrier(0);
+        a = xs4[(kb + 1) * (XS_BLOCK / 4)];
+        if (PRIO == 1) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+            for (int t = 0; t < TPW; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s], b1[t][s], acc[t], 0, 0, 0);
+        if (PRIO == 1) __builtin_amdgcn_s_setprio(0);
+        const int k3 = kb + 3 < NK8 ? kb + 3 : NK8 - 1;
+#pragma unroll
+        for (int t = 0; t < TPW; ++t) b1[t] = ld(t, k3);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    if (PRIO == 2) __builtin_amdgcn_s_setprio(0);
+}
+
+// 4-register ring, loads issued AFTER each k-block's MFMAs (2 k-blocks of cover)
+template <int TPW>
+__device__ __forceinline__ void gemm_ring_after(const float* Xs, const float* alpha_sw, floatx16 (&acc)[TPW]) {
+    constexpr int N = TPW * 256, NK8 = N / 8, TSTRIDE = NK8 * 64;
+    int lane;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    for (int t = 0; t < TPW; ++t)
+        for (int r = 0; r < 16; ++r) acc[t][r] = 0.0f;
+    const floatx4* xs4 = reinterpret_cast<const floatx4*>(Xs + (lane >> 5) * XS_HALF + (lane & 31) * 4);
+    gfloatx4* bp = (gfloatx4*)(alpha_sw) + (size_t)(wave * TPW) * TSTRIDE + lane;
+    floatx4 b[4][TPW];
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+#pragma unroll
+        for (int t = 0; t < TPW; ++t) b[j][t] = bp[t * TSTRIDE + j * 64];
+#pragma unroll 1
+    for (int kb = 0; kb < NK8; kb += 4) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const floatx4 a = xs4[(kb + u) * (XS_BLOCK / 4)];
+#pragma unroll
+            for (int s = 0; s < 4; ++s)
+#pragma unroll
+                for (int t = 0; t < TPW; ++t)
+                    acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s], b[u][t][s], acc[t], 0, 0, 0);
+            const int kn = kb + u + 3 < NK8 ? kb + u + 3 : NK8 - 1;
+#pragma unroll
+            for (int t = 0; t < TPW; ++t) b[(u + 3) & 3][t] = bp[t * TSTRIDE + kn * 64];
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+}
+
+template <int V, int TPW, int SCHED_>
+__global__ __launch_bounds__(NTHREADS) void gemm_kernel(const float* alpha_sw, float* out, int reps) {
+    extern __shared__ float Xs[];
+    constexpr int N = TPW * 256;
+    for (int i = threadIdx.x; i < xs_floats(N); i += blockDim.x) Xs[i] = 1e-3f * (float)((i * 7 + blockIdx.x) & 15);
+    __syncthreads();
+    float sink = 0.0f;
+    for (int r = 0; r < reps; ++r) {
+        floatx16 acc[TPW];
+        if (V == 0) {
+            gemm_v0<TPW, SCHED_>(Xs, alpha_sw, acc);
+        } else if (V == 2) {
+            gemm_v0<TPW, 1, 1>(Xs, alpha_sw, acc);
+        } else if (V == 3) {
+            gemm_v0<TPW, 1, 2>(Xs, alpha_sw, acc);
+        } else if (V == 4) {
+            gemm_v2<TPW, 1, 0>(Xs, alpha_sw, acc);
+        } else if (V == 5) {
+            gemm_v2<TPW, 2, 0>(Xs, alpha_sw, acc);
+        } else if (V == 6) {
+            gemm_v2<TPW, 0, 1>(Xs, alpha_sw, acc);
+        } else if (V == 8) {
+            gemm_v2<TPW, 1, 1>(Xs, alpha_sw, acc);
+        } else if (V == 9) {
+            gemm_v2<TPW, 2, 1>(Xs, alpha_sw, acc);
+        } else if (V == 7) {
+            gemm_ring_after<TPW>(Xs, alpha_sw, acc);
+        } else {
+            coupling_gemm<TPW>(Xs, alpha_sw, acc);
+        }
+        for (int t = 0; t < TPW; ++t) sink += acc[t][r & 15];
+        lds_barrier();
+    }
+    out[blockIdx.x * blockDim.x + threadIdx.x] = sink;
+}
+
+template <int V, int S>
+static double run(const float* dA, float* dO, int nwg, int reps) {
+    constexpr int TPW = 4, N = 1024;
+    const size_t lds = (size_t)xs_floats(N) * 4;
+    hipFuncSetAttribute((const void*)gemm_kernel<V, TPW, S>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);  // NOLINT
+    hipLaunchKernelGGL((gemm_kernel<V, TPW, S>), dim3(nwg), dim3(NTHREADS), lds, 0, dA, dO, 2);
+    hipEvent_t e0, e1;
+    hipEventCreate(&e0);
+    hipEventCreate(&e1);
+    hipEventRecord(e0, 0);
+    hipLaunchKernelGGL((gemm_kernel<V, TPW, S>), dim3(nwg), dim3(NTHREADS), lds, 0, dA, dO, reps);
+    hipEventRecord(e1, 0);
+    hipEventSynchronize(e1);
+    float ms = 0;
+    hipEventElapsedTime(&ms, e0, e1);
+    const double flop = (double)nwg * reps * 32.0 * N * N * 2.0;
+    return flop / (ms * 1e-3) / 1e12;
+}
+
+
+// ---- 16x16x4 variant: two independent 8-env groups per workgroup ----------
+// waves 0-3 = group 0, waves 4-7 = group 1; each wave owns 16 column tiles of
+// 16 (all 1024 columns / 4 waves); A = 16 rows (8 envs x sin/cos) per group.
+template <int NT>
+__global__ __launch_bounds__(NTHREADS) void gemm16_kernel(const float* alpha_sw, float* out, int reps) {
+    extern __shared__ float Xs[];
+    constexpr int N = 1024, NKB = N / 16;  // 16-k blocks
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, grp = wave >> 2, wg = wave & 3;
+    for (int i = threadIdx.x; i < 2 * NKB * 64 * 4; i += blockDim.x) Xs[i] = 1e-3f * (float)((i * 7 + blockIdx.x) & 15);
+    __syncthreads();
+    const floatx4* xa = reinterpret_cast<const floatx4*>(Xs) + grp * NKB * 64 + lane;
+    // B tiles: [tile 0..63][kb 0..63][lane] float4; wave's tiles = 16*wg .. 16*wg+15
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)(alpha_sw + (size_t)wg * 16 * NKB * 64 * 4), 0, 16 * NKB * 64 * 16, 0x00020000);
+    auto ld = [&](int t, int k) -> floatx4 {
+        return __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(rs, (lane + k * 64) * 16, t * NKB * 64 * 16, 0));
+    };
+    float sink = 0.0f;
+    for (int r = 0; r < reps; ++r) {
+        floatx4 acc[16];
+        for (int t = 0; t < 16; ++t) acc[t] = floatx4{0, 0, 0, 0};
+        floatx4 b0[8], b1[8];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) { b0[t] = ld(t, 0); b1[t] = ld(8 + t, 0); }
+#pragma unroll 1
+        for (int kb = 0; kb < NKB; ++kb) {
+            const floatx4 a = xa[kb * 64];
+            const int kn = kb + 1 < NKB ? kb + 1 : NKB - 1;
+#pragma unroll
+            for (int s2 = 0; s2 < 4; ++s2)
+#pragma unroll
+                for (int t = 0; t < 8; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s2], b0[t][s2], acc[t], 0, 0, 0);
+#pragma unroll
+            for (int t = 0; t < 8; ++t) b0[t] = ld(t, kn);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int s2 = 0; s2 < 4; ++s2)
+#pragma unroll
+                for (int t = 0; t < 8; ++t) acc[8 + t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s2], b1[t][s2], acc[8 + t], 0, 0, 0);
+#pragma unroll
+            for (int t = 0; t < 8; ++t) b1[t] = ld(8 + t, kn);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        for (int t = 0; t < 16; ++t) sink += acc[t][r & 3];
+        lds_barrier();
+    }
+    out[blockIdx.x * blockDim.x + threadIdx.x] = sink;
+}
+
+static double run16(const float* dA, float* dO, int nwg, int reps) {
+    const size_t lds = (size_t)2 * 64 * 64 * 4 * 4;
+    hipFuncSetAttribute((const void*)gemm16_kernel<16>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);  // NOLINT
+    hipLaunchKernelGGL(gemm16_kernel<16>, dim3(nwg), dim3(NTHREADS), lds, 0, dA, dO, 2);
+    hipEvent_t e0, e1;
+    hipEventCreate(&e0);
+    hipEventCreate(&e1);
+    hipEventRecord(e0, 0);
+    hipLaunchKernelGGL(gemm16_kernel<16>, dim3(nwg), dim3(NTHREADS), lds, 0, dA, dO, reps);
+    hipEventRecord(e1, 0);
+    hipEventSynchronize(e1);
+    float ms = 0;
+    hipEventElapsedTime(&ms, e0, e1);
+    const double flop = (double)nwg * reps * 32.0 * 1024 * 1024 * 2.0;  // 2 groups x 16 rows
+    return flop / (ms * 1e-3) / 1e12;
+}
+
+// exactness probe: one 16x16 tile, K=64, 16x16x4 MFMA chain vs sequential fmaf
+__global__ void mfma16_probe(const float* A, const float* Bm, float* C) {
+    const int lane = threadIdx.x;
+    floatx4 acc = {0, 0, 0, 0};
+    for (int k4 = 0; k4 < 16; ++k4) {
+        const int k = 4 * k4 + (lane >> 4);
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(A[(lane & 15) * 64 + k], Bm[k * 16 + (lane & 15)], acc, 0, 0, 0);
+    }
+    for (int j = 0; j < 4; ++j) C[(4 * (lane >> 4) + j) * 16 + (lane & 15)] = acc[j];
+}
+
+static int probe16() {
+    std::vector<float> A(16 * 64), Bm(64 * 16), C(256), R(256), R2(256);
+    unsigned s = 12345;
+    auto rnd = [&]() { s = s * 1664525u + 1013904223u; return ((s >> 8) & 0xffff) / 32768.0f - 1.0f; };
+    for (auto& x : A) x = rnd() * 3.1f;
+    for (auto& x : Bm) x = rnd() * 0.9f;
+    float *dA, *dB, *dC;
+    hipMalloc(&dA, A.size() * 4); hipMalloc(&dB, Bm.size() * 4); hipMalloc(&dC, 256 * 4);
+    hipMemcpy(dA, A.data(), A.size() * 4, hipMemcpyHostToDevice);
+    hipMemcpy(dB, Bm.data(), Bm.size() * 4, hipMemcpyHostToDevice);
+    hipLaunchKernelGGL(mfma16_probe, dim3(1), dim3(64), 0, 0, dA, dB, dC);
+    hipMemcpy(C.data(), dC, 256 * 4, hipMemcpyDeviceToHost);
+    int bad = 0, bad2 = 0;
+    for (int m = 0; m < 16; ++m)
+        for (int n = 0; n < 16; ++n) {
+            float a = 0.0f;
+            for (int k = 0; k < 64; ++k) a = fmaf(A[m * 64 + k], Bm[k * 16 + n], a);
+            R[m * 16 + n] = a;
+            // hypothesis 2: per 4-k step, exact dot of 4 products then one rounding into acc
+            double acc = 0.0; float af = 0.0f;
+            for (int k4 = 0; k4 < 16; ++k4) {
+                double d = (double)af;
+                for (int j = 0; j < 4; ++j) d += (double)A[m * 64 + 4 * k4 + j] * (double)Bm[(4 * k4 + j) * 16 + n];
+                af = (float)d;
+            }
+            (void)acc;
+            R2[m * 16 + n] = af;
+            bad += C[m * 16 + n] != R[m * 16 + n];
+            bad2 += C[m * 16 + n] != R2[m * 16 + n];
+        }
+    printf("\"mfma16_mismatch_vs_fmaf_chain\": %d, \"mfma16_mismatch_vs_dot4_round\": %d, ", bad, bad2);
+    return bad;
+}
+
+int main() {
+    const int N = 1024, nwg = 256, reps = 200;
+    float *dA, *dO;
+    hipMalloc(&dA, (size_t)N * N * 4);
+    hipMalloc(&dO, (size_t)nwg * NTHREADS * 4);
+    std::vector<float> h((size_t)N * N);
+    for (size_t i = 0; i < h.size(); ++i) h[i] = 1e-3f * (float)(i % 97);
+    hipMemcpy(dA, h.data(), h.size() * 4, hipMemcpyHostToDevice);
+    printf("{");
+    probe16();
+    printf("\"gemm16_two_groups\": %.2f, ", run16(dA, dO, nwg, reps));
+    printf("\"v0_two_buffers\": %.2f, ", run<0, 0>(dA, dO, nwg, reps));
+    printf("\"v0_two_buffers_sched\": %.2f, ", run<0, 1>(dA, dO, nwg, reps));
+    printf("\"v0_sched_small_alpha_set\": %.2f, ", run<2, 0>(dA, dO, nwg, reps));
+    printf("\"v0_sched_no_alpha_loads\": %.2f, ", run<3, 0>(dA, dO, nwg, reps));
+    printf("\"prio_clusters\": %.2f, ", run<4, 0>(dA, dO, nwg, reps));
+    printf("\"prio_static_upper_half\": %.2f, ", run<5, 0>(dA, dO, nwg, reps));
+    printf("\"buffer_loads\": %.2f, ", run<6, 0>(dA, dO, nwg, reps));
+    printf("\"ring4_loads_after\": %.2f, ", run<7, 0>(dA, dO, nwg, reps));
+    printf("\"buffer_prio_clusters\": %.2f, ", run<8, 0>(dA, dO, nwg, reps));
+    printf("\"buffer_prio_static\": %.2f, ", run<9, 0>(dA, dO, nwg, reps));
+    printf("\"production\": %.2f, \"unit\": \"TFLOP/s\", \"peak\": 157.3}\n", run<1, 0>(dA, dO, nwg, reps));
+    return 0;
+}

@@ -1,0 +1,18 @@
+# rocprofv3 evidence for the bench kernel (run on the GPU box via gpurun):
+#   bash tools/rocprof_run.sh <outname>
+# 1) kernel trace + stats of a short bench run (average kernel duration must
+#    agree with bench.py's HIP-event figure);
+# 2) FETCH_SIZE and 3) WRITE_SIZE in separate --pmc passes (MI355X guide: the
+#    two do not fit one TCC pass; FETCH_SIZE is doubled for 16 B/lane loads).
+set -e
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+O=$R/gpurun_out/${1:-prof}
+mkdir -p $O
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o run -- \
+    python3 $R/bench.py --steps 10 --warmup 2 --cpu-seconds 0 > $O/bench_trace.json 2> $O/trace.err
+timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/fetch -o run -- \
+    python3 $R/bench.py --steps 3 --warmup 1 --cpu-seconds 0 > $O/bench_fetch.json 2> $O/fetch.err
+timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/write -o run -- \
+    python3 $R/bench.py --steps 3 --warmup 1 --cpu-seconds 0 > $O/bench_write.json 2> $O/write.err
+echo DONE
