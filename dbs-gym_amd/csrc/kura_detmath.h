@@ -48,24 +48,35 @@
 // For |y| < 2^22 the quotient estimate is off by at most one and the
 // remainder computed by fmaf is exact; larger |y| takes the
 // classic shift-subtract path, which is exact by Sterbenz's lemma.
-KDM_FN float kdm_fmod2pi(float y) {
+// Fast path of kdm_fmod2pi, exact for |y| < 2^22 (sets *slow otherwise; the
+// caller then re-evaluates that element with kdm_fmod2pi).  Branch-free, so a
+// batch of elements keeps its instruction-level parallelism.
+KDM_FN float kdm_fmod2pi_fast(float y, int* slow) {
     const float d = KDM_TWO_PI_F;
     const float ay = fabsf(y);
-    // fast path (|y| < 2^22), branch-free: exact remainder by fmaf, one fix-up
     const float q = truncf(ay * KDM_INV_TWO_PI_F);
     float r = KDM_FMAF(-q, d, ay);
     r = r < 0.0f ? r + d : r;
     r = r >= d ? r - d : r;
-    if (!(ay < 4194304.0f)) {  // rare: shift-subtract long division
-        r = ay;
-        if (!(r < 3.0e38f)) return (y - y) / (y - y);  // inf/nan -> nan
-        float dd = d;
-        int e = 0;
-        while (dd * 2.0f <= r) { dd *= 2.0f; ++e; }
-        for (; e >= 0; --e) {
-            if (r >= dd) r -= dd;
-            dd *= 0.5f;
-        }
+    *slow |= !(ay < 4194304.0f);
+    return y < 0.0f ? -r : r;
+}
+
+KDM_FN float kdm_fmod2pi(float y) {
+    int slow = 0;
+    const float rf = kdm_fmod2pi_fast(y, &slow);
+    if (!slow) return rf;
+    // rare (|y| >= 2^22, inf, nan): shift-subtract long division, exact by
+    // Sterbenz's lemma
+    const float d = KDM_TWO_PI_F;
+    float r = fabsf(y);
+    if (!(r < 3.0e38f)) return (y - y) / (y - y);  // inf/nan -> nan
+    float dd = d;
+    int e = 0;
+    while (dd * 2.0f <= r) { dd *= 2.0f; ++e; }
+    for (; e >= 0; --e) {
+        if (r >= dd) r -= dd;
+        dd *= 0.5f;
     }
     return y < 0.0f ? -r : r;
 }
@@ -94,6 +105,7 @@ KDM_FN void kdm_sincosf(float x, float* s_out, float* c_out) {
     *s_out = s;
     *c_out = c;
 }
+
 
 KDM_FN float kdm_cosf(float x) {
     float s, c;

@@ -2,18 +2,20 @@
 // environment: one launch = one SpatialKuramoto.step() (env.py:415-454) or
 // one reset() transient (env.py:594-614) for every environment of a handle.
 //
-// Work decomposition (DESIGN.md "Kernel K1"):
+// Work decomposition:
 //   * one workgroup = 16 environments (E_WG), 512 threads = 8 wavefronts;
 //   * the O(N^2) coupling of one RHS sweep is the GEMM
 //         [sin theta ; cos theta] (32 x N)  x  alpha^T (N x N)
 //     on v_mfma_f32_32x32x2_f32 (exact fp32, k-ordered fmaf chain), with the
-//     32 x N operand resident in LDS (128 KiB at N=1024) in MFMA fragment order
-//     and alpha streamed from L2/MALL in a host-swizzled fragment layout;
-//   * every element-wise / reduction stage (Dopri5 stage inputs, error norm,
-//     dense output, LFP, window, reward) runs in the "R64" layout: wave w owns
-//     envs {2w, 2w+1}, lane l owns oscillators l, l+64, ...  so each per-env
-//     sum is a strided lane loop + xor butterfly (kura_detmath.h), identical
-//     to the CPU oracle's order.
+//     32 x N operand resident in LDS (132 KiB at N=1024) in MFMA fragment order
+//     and alpha streamed from L2/MALL in a host-swizzled fragment layout
+//     through raw buffer loads;
+//   * every element-wise stage (Dopri5 stage inputs, coupling epilogue, error
+//     norm, dense output + LFP, FSAL) runs in the MFMA accumulator layout:
+//     wave w owns column tiles w*TPW .. w*TPW+TPW-1 for all 16 envs, and its
+//     solver records ([slot][N][16 envs] in HBM) are only ever touched by the
+//     lane that owns them; sums over oscillators use the RM order and sums
+//     over the window the R64 order (kura_detmath.h).
 // The arithmetic is a bit-exact twin of oracle/kura_oracle.c; this file must
 // be compiled with -ffp-contract=off (see __graft_entry__.build).
 #include <hip/hip_runtime.h>
@@ -238,9 +240,6 @@ __device__ __forceinline__ void coupling_gemm(const float* __restrict__ Xs, cons
         for (int t = 0; t < TPW; ++t) b1[t] = ld(t, k3);
         __builtin_amdgcn_sched_barrier(0);
     }
-#ifdef KURA_GEMM_NOPS
-    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
-#endif
 }
 
 // Workgroup barrier that orders LDS only.  Inside a solve every workspace
@@ -249,10 +248,6 @@ __device__ __forceinline__ void coupling_gemm(const float* __restrict__ Xs, cons
 // outstanding global store and load (vmcnt(0)) -- is not needed there; only
 // LDS (the GEMM operand, control slots, reduction partials) is shared.
 __device__ __forceinline__ void lds_barrier() {
-#ifdef KURA_FULL_BARRIER
-    __syncthreads();
-    return;
-#endif
     // compiler-only barrier for the records: they are stored through global
     // pointers and loaded through a buffer descriptor, and nothing may be
     // reordered across a phase boundary
@@ -365,11 +360,9 @@ template <int TPW>
 __device__ __forceinline__ void coupling_epilogue(const DevParams& p, const Slot& ws, const float* __restrict__ Xs,
                                                   const floatx16 (&acc)[TPW], int stage, bool pulse_on) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int hq = lane >> 5;
     float w[TPW][8], u[TPW][8];
 #pragma unroll
     for (int t = 0; t < TPW; ++t) {
-        const int i = 32 * (wave * TPW + t) + (lane & 31);
         load8(ws, SL_W, t, w[t]);
         if (pulse_on) {
             load8(ws, SL_P, t, u[t]);
@@ -402,21 +395,19 @@ __device__ __forceinline__ void coupling_epilogue(const DevParams& p, const Slot
 template <int NT>
 __device__ __forceinline__ void stage_tiles(const Slot& ws, float* Xs, int s, const float (&h)[8], int t0) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int hq = lane >> 5;
     const int TPW = ws.N / 256;
     float y0[NT][8], f[NT][6][8];
 #pragma unroll
     for (int u = 0; u < NT; ++u) {
-        const int i = 32 * (wave * TPW + t0 + u) + (lane & 31);
         load8(ws, SL_Y0, t0 + u, y0[u]);
 #pragma unroll
         for (int j = 0; j < 6; ++j)
             if (j < s) load8(ws, SL_F0 + j, t0 + u, f[u][j]);
     }
+    float ys[NT][8], th[NT][8];
+    int slow = 0;
 #pragma unroll
     for (int u = 0; u < NT; ++u) {
-        const int i = 32 * (wave * TPW + t0 + u) + (lane & 31);
-        float ys[8];
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
             float v = y0[u][q];
@@ -429,14 +420,28 @@ __device__ __forceinline__ void stage_tiles(const Slot& ws, float* Xs, int s, co
                 if (s > 5) acc = __builtin_fmaf(cA[s][5], h[q] * f[u][5][q], acc);
                 v = y0[u][q] + acc;
             }
-            ys[q] = v;
+            ys[u][q] = v;
+            th[u][q] = kdm_fmod2pi_fast(v, &slow);
+        }
+    }
+    if (__builtin_expect(__any(slow), 0)) {  // |y| >= 2^22: never in practice
+#pragma unroll
+        for (int u = 0; u < NT; ++u)
+#pragma unroll
+            for (int q = 0; q < 8; ++q) th[u][q] = kdm_fmod2pi(ys[u][q]);
+    }
+#pragma unroll
+    for (int u = 0; u < NT; ++u) {
+        const int i = 32 * (wave * TPW + t0 + u) + (lane & 31);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
             float sn, cs;
-            kdm_sincosf(kdm_fmod2pi(v), &sn, &cs);
+            kdm_sincosf(th[u][q], &sn, &cs);
             const int e = mfma_env(q, lane);
             Xs[xs_idx(e, i)] = sn;
             Xs[xs_idx(16 + e, i)] = cs;
         }
-        if (s == 6) store8(ws, SL_Y1, t0 + u, ys);
+        if (s == 6) store8(ws, SL_Y1, t0 + u, ys[u]);
     }
 }
 
@@ -492,7 +497,6 @@ __device__ __forceinline__ double rm_total_d(int e, int k) {
 template <int TPW>
 __device__ __forceinline__ void post_step(const DevParams& p, const Slot& ws, int env_base, bool to_ring STAMP_PARAMS) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, tid = threadIdx.x;
-    const int hq = lane >> 5;
     constexpr int N = TPW * 256;
     float h[8];
 #pragma unroll
@@ -501,7 +505,6 @@ __device__ __forceinline__ void post_step(const DevParams& p, const Slot& ws, in
     float part[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll 1
     for (int t = 0; t < TPW; ++t) {
-        const int i = 32 * (wave * TPW + t) + (lane & 31);
         float y0[8], y1[8], f0[8], f2[8], f3[8], f4[8], f5[8], f6[8];
         load8(ws, SL_Y0, t, y0);
         load8(ws, SL_Y1, t, y1);
@@ -698,7 +701,6 @@ __device__ __forceinline__ void post_step(const DevParams& p, const Slot& ws, in
     for (int q = 0; q < 8; ++q) kp[q] = s_ctl[mfma_env(q, lane)].keep;
 #pragma unroll 1
     for (int t = 0; t < TPW; ++t) {
-        const int i = 32 * (wave * TPW + t) + (lane & 31);
         float y0[8], y1[8], f0[8], f6[8];
         load8(ws, SL_Y0, t, y0);
         load8(ws, SL_Y1, t, y1);
