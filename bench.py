@@ -42,6 +42,7 @@ def parse():
     ap.add_argument("--reward", default="bbpow_action")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline sample (0 = skip)")
     ap.add_argument("--seed", type=int, default=2024)
+    ap.add_argument("--random-k", action="store_true", help="per-env K ~ U(0.3, 0.8) (north_star 'random K')")
     return ap.parse_args()
 
 
@@ -55,16 +56,18 @@ def build_shard(args, rank):
         gid = rank * B + b
         p = dict(base)
         p["rand_seed"] = args.seed + gid
+        if args.random_k:
+            p["K"] = float(np.random.default_rng(args.seed * 7919 + gid).uniform(0.3, 0.8))
         plist.append(kura.fill_driver_arrays(p, w0_seed=10_000_000 + args.seed + gid))
     hosts, shared = kura.build_batch(plist)
     omega, g_stim, g_rec, theta0 = kura.reset_arrays(hosts)
     cfg = sim_mod.make_config(base, B, reward_func=args.reward)
     bins = kura.spectral.beta_bins(cfg.window, base["verbose_dt"])
     ctab, stab = kura.spectral.twiddles(cfg.window, bins)
-    return cfg, shared["alpha"].astype(np.float32), omega, g_stim, g_rec, theta0, ctab, stab
+    return cfg, shared["alpha"].astype(np.float32), omega, g_stim, g_rec, theta0, ctab, stab, shared["gain"]
 
 
-def cpu_baseline(args, cfg, alpha, omega, g_stim, g_rec, theta0, ctab, stab):
+def cpu_baseline(args, cfg, alpha, omega, g_stim, g_rec, theta0, ctab, stab, gain):
     """The oracle (CPU restatement of step()) on this host's cores, bounded sample."""
     from oracle import kura_oracle as ko
     import copy
@@ -75,6 +78,7 @@ def cpu_baseline(args, cfg, alpha, omega, g_stim, g_rec, theta0, ctab, stab):
     c.n_envs = nb
     o = ko.Oracle(c, alpha)
     o.set_env_params(omega[:nb], g_stim[:nb], g_rec[:nb])
+    o.set_gain(gain[:nb])
     o.set_spectral(ctab, stab)
     o.reset(theta0[:nb])
     rng = np.random.default_rng(0)
@@ -129,9 +133,10 @@ def main():
 
     sim_mod = importlib.import_module("dbs-gym_amd.sim")
     t_setup = time.perf_counter()
-    cfg, alpha, omega, g_stim, g_rec, theta0, ctab, stab = build_shard(args, rank)
+    cfg, alpha, omega, g_stim, g_rec, theta0, ctab, stab, gain = build_shard(args, rank)
     sim = sim_mod.KuraSim(cfg, local_rank)
     sim.set_coupling(alpha)
+    sim.set_env_gain(gain)
     sim.set_env_params(omega, g_stim, g_rec)
     sim.set_spectral(ctab, stab)
     t_setup = time.perf_counter() - t_setup
@@ -207,7 +212,8 @@ def main():
             "dtype": "f32",
             "data": "synthetic (seeded reference-sampler natural frequencies, N(pi,0.6) phases, U(-1,1) actions)",
             "config": {"workload": f"{args.config} reference step(), N={N} oscillators x {B} envs per GPU, "
-                                   f"adaptive Dopri5 rtol=atol=1e-5, W={cfg.window}, reward={args.reward}",
+                                   f"adaptive Dopri5 rtol=atol=1e-5, W={cfg.window}, reward={args.reward}"
+                                   + (", per-env K~U(0.3,0.8)" if args.random_k else ", K=0.52"),
                        "global_envs": world * B, "parallelism": f"env-shard x{world} (no collectives)"},
             "roofline": {"bound": "mfma", "achieved": achieved_tf, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
                          "frac": achieved_tf / PEAK_FP32_TFLOPS, "traffic": traffic,
@@ -223,7 +229,7 @@ def main():
                       "host_setup_s": t_setup},
         }
         if world == 1 and args.cpu_seconds > 0:
-            out["cpu_baseline"] = cpu_baseline(args, cfg, alpha, omega, g_stim, g_rec, theta0, ctab, stab)
+            out["cpu_baseline"] = cpu_baseline(args, cfg, alpha, omega, g_stim, g_rec, theta0, ctab, stab, gain)
         else:
             out["cpu_baseline"] = None
         print(json.dumps(out), flush=True)

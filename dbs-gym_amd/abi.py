@@ -91,6 +91,7 @@ _SYMBOLS = {
     "kura_reward": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p]),
     "kura_get_state": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "kura_set_state": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "kura_set_env_gain": (c_int, [c_void_p, c_int, c_int, c_void_p]),
     "kura_get_stats": (c_int, [c_void_p, c_void_p, c_int]),
     "kura_get_stamps": (c_int, [c_void_p, c_void_p]),
     "kura_selftest_math": (c_int, [c_void_p, c_void_p, c_void_p, c_int]),

@@ -127,17 +127,19 @@ def fill_driver_arrays(params: dict, w0_seed: int | None = None, rs: np.random.R
 
 
 def build_batch(params_list: list[dict]) -> tuple[list[EnvHost], dict]:
-    """Host setup for B envs sharing N and the grid: returns the EnvHost list and
-    the shared coupling alpha (float64, env.py:219-229)."""
+    """Host setup for B envs sharing N, the grid and the spatial kernel: returns
+    the EnvHost list and the shared coupling alpha (float64, env.py:219-229).
+    K may differ per env (its float32(K/N) gain goes to kura_set_env_gain)."""
     hosts = [EnvHost(p) for p in params_list]
     p0 = params_list[0]
     for p in params_list[1:]:
         if p["num_oscillators"] != p0["num_oscillators"] or list(p["grid_size"]) != list(p0["grid_size"]):
             raise ValueError("all envs of a batch must share N and the grid")
-        if p["K"] != p0["K"] or p["spatial_kernel"] != p0["spatial_kernel"]:
-            raise ValueError("all envs of a batch must share the coupling (K, spatial kernel)")
+        if p["spatial_kernel"] != p0["spatial_kernel"]:
+            raise ValueError("all envs of a batch must share the spatial coupling kernel")
     alpha = ms.coupling_alpha(p0["neur_coords"], p0["spatial_kernel"], p0["wavelet_amp"], p0["wavelet_steepness"])
-    return hosts, {"alpha": alpha}
+    gains = np.array([np.float32(p["K"] / p["num_oscillators"]) for p in params_list], np.float32)  # env.py:264
+    return hosts, {"alpha": alpha, "gain": gains}
 
 
 def reset_arrays(hosts: list[EnvHost], idx=None):

@@ -76,6 +76,7 @@ struct DevParams {
     float rtol, atol, kn, dt0;
     const float* alpha_sw;  // B-fragment swizzled coupling
     const float* omega;     // [B][N]
+    const float* kn_env;    // [B] float32(K_b / N), per-env coupling gain
     const double* g_stim;   // [B][n_elec][N]
     const double* g_rec;    // [B][N] recorder conductance sum G = g_0 + g_1 + ... (host-summed)
     const double* ctab;     // [n_bins][W]
@@ -272,6 +273,7 @@ struct CtlE {
     float t1, tprev, tnext, h, dtn;
 };
 __shared__ CtlE s_ctl[E_WG];
+__shared__ float s_kn[E_WG];  // per-env coupling gain of the workgroup's envs
 #define RC 4  // save rounds evaluated per pass over the records
 __shared__ float s_red[RC][NWAVES][E_WG];        // per-wave partial sums (f32)
 __shared__ double s_redd[RC][NWAVES][E_WG];      // per-wave partial sums (f64, recorder LFP)
@@ -371,6 +373,9 @@ __device__ __forceinline__ void coupling_epilogue(const DevParams& p, const Slot
             for (int q = 0; q < 8; ++q) u[t][q] = 0.0f;  // still added: x + 0 is not folded (signed zeros)
         }
     }
+    float knq[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) knq[q] = s_kn[mfma_env(q, lane)];
 #pragma unroll
     for (int t = 0; t < TPW; ++t) {
         const int i = 32 * (wave * TPW + t) + (lane & 31);
@@ -382,7 +387,7 @@ __device__ __forceinline__ void coupling_epilogue(const DevParams& p, const Slot
             const float sn = Xs[xs_idx(e, i)], cs = Xs[xs_idx(16 + e, i)];
             const float tq = sn * Q;
             const float coup = __builtin_fmaf(cs, P, -tq);
-            f[q] = __builtin_fmaf(p.kn, coup, w[t][q]) + u[t][q];
+            f[q] = __builtin_fmaf(knq[q], coup, w[t][q]) + u[t][q];
         }
         store8(ws, SL_F0 + stage, t, f);
     }
@@ -771,6 +776,10 @@ __device__ void solve_wg(const DevParams& p, float* Xs, int env_base, bool to_ri
         if (pulse_on) store8(ws, SL_P, t, u);
     }
     asm volatile("" ::: "memory");  // record stores before the first record loads
+    if (tid < E_WG) {  // visible to the epilogue after the first stage barrier
+        const int env = env_base + tid;
+        s_kn[tid] = p.kn_env[env < p.B ? env : p.B - 1];
+    }
     STAMP_DECL
     long long nrhs = 0;
     int s = 0;  // stage 0 = initial RHS at y0 (FSAL seed)

@@ -111,6 +111,11 @@ class KuraSim:
                                                      None if gr is None else gr.ctypes.data),
               "kura_set_env_params")
 
+    def set_env_gain(self, kn, env0: int = 0) -> None:
+        """Per-env coupling gain float32(K_b / N) (env.py:264)."""
+        k = np.ascontiguousarray(kn, dtype=np.float32).reshape(-1)
+        check(self.lib, self.lib.kura_set_env_gain(self._h, env0, len(k), k.ctypes.data), "kura_set_env_gain")
+
     def set_spectral(self, cos_tab, sin_tab) -> None:
         c = np.ascontiguousarray(cos_tab, dtype=np.float64)
         s = np.ascontiguousarray(sin_tab, dtype=np.float64)

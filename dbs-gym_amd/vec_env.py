@@ -43,7 +43,8 @@ class KuraVectorEnv:
     """B SpatialKuramoto environments stepped together on one GPU.
 
     params:     one reference params dict for every env, or a list of B dicts
-                (they must share N, the grid, K and the spatial kernel).
+                (they must share N, the grid and the spatial kernel; K may
+                differ per env).
                 Driver-filled arrays (w0, neur_coords, ...) may be given; when
                 absent they are drawn as train_aDBS_RL.py:95-112 does, from
                 ``numpy.random.RandomState(w0_seed + b)``.
@@ -81,6 +82,7 @@ class KuraVectorEnv:
         self.sim = KuraSim(self.cfg, device)
         self.device = self.sim.device
         self.sim.set_coupling(shared["alpha"].astype(np.float32))
+        self.sim.set_env_gain(shared["gain"])                      # per-env K (env.py:264)
         bins = spectral.beta_bins(self.cfg.window, plist[0]["verbose_dt"])
         self.sim.set_spectral(*spectral.twiddles(self.cfg.window, bins))
         self.W, self.N, self.n_elec = self.cfg.window, self.cfg.n_osc, self.cfg.n_elec

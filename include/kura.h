@@ -17,6 +17,7 @@
  *   kura_create          SpatialKuramoto.__init__        env.py:277-386
  *   kura_set_coupling    KuramotoJAX.__init__ alpha     env.py:219-229
  *   kura_set_env_params  apply_locus_mask + SimpleDBS    env.py:566-593, :61-156
+ *   kura_set_env_gain    KuramotoJAX(K=...) per env      env.py:264, :570-593
  *   kura_set_spectral    calc_beta_band_power bins       utils.py:21-27
  *   kura_reset           SpatialKuramoto.reset transient env.py:594-614
  *   kura_step            SpatialKuramoto.step            env.py:415-454
@@ -94,6 +95,10 @@ int kura_set_env_params(KuraHandle* h, int env0, int n,
                         const float* omega,   /* n*N  (float32 cast of w0, env.py:264) */
                         const double* g_stim, /* n*n_elec*N conductances, env.py:106-120 */
                         const double* g_rec); /* n*n_rec*N  recorder conductances, :142-156 */
+/* per-env coupling gain float32(K_b / N) for envs [env0, env0+n) (host
+ * array; each reference env has its own params_dict['K'], env.py:264).  Envs
+ * not set keep the config's kn. */
+int kura_set_env_gain(KuraHandle* h, int env0, int n, const float* kn);
 int kura_set_spectral(KuraHandle* h, const double* cos_tab, const double* sin_tab /* n_bins*W */);
 
 /* hot path (device pointers, asynchronous on stream) */

@@ -187,7 +187,11 @@ typedef struct {
     KuraConfig cfg;
     int N;
     float* alphaT; /* alphaT[j*N + i] = alpha[i][j] */
+    float* kn_env; /* per-env float32(K/N) (oracle_set_gain), NULL -> cfg.kn */
+    int kn_n;
 } OCtx;
+
+static float kn_of(const OCtx* o, int b) { return (o->kn_env && b < o->kn_n) ? o->kn_env[b] : o->cfg.kn; }
 
 void* oracle_create(const KuraConfig* cfg, const float* alpha) {
     OCtx* o = (OCtx*)calloc(1, sizeof(OCtx));
@@ -206,7 +210,20 @@ void oracle_destroy(void* p) {
     OCtx* o = (OCtx*)p;
     if (!o) return;
     free(o->alphaT);
+    free(o->kn_env);
     free(o);
+}
+
+/* Per-env coupling gain float32(K_b / N) (each env's params_dict['K'],
+ * env.py:264); envs beyond n keep cfg.kn. */
+int oracle_set_gain(void* ctx, int n, const float* kn) {
+    OCtx* o = (OCtx*)ctx;
+    free(o->kn_env);
+    o->kn_env = (float*)malloc(sizeof(float) * (size_t)(n > 0 ? n : 1));
+    if (!o->kn_env) return KURA_E_NOMEM;
+    memcpy(o->kn_env, kn, sizeof(float) * (size_t)n);
+    o->kn_n = n;
+    return KURA_OK;
 }
 
 /* Work buffers for one env (one OpenMP thread). */
@@ -219,6 +236,7 @@ typedef struct {
     float *cosrow;
     float *zero;          /* pulse = 0 (stim OFF), env.py:434 */
     double *prod;
+    float kn;             /* coupling gain of the env being solved */
 } Work;
 
 static int work_alloc(Work* w, int N) {
@@ -272,7 +290,7 @@ static void rhs(const OCtx* o, Work* w, const float* y, const float* omega, cons
         }
         for (int i = ib; i < ie; ++i) { w->P[i] = Pb[i - ib]; w->Q[i] = Qb[i - ib]; }
     }
-    const float kn = o->cfg.kn;
+    const float kn = w->kn;
     for (int i = 0; i < N; ++i) {
         float t = w->s[i] * w->Q[i];
         float coup = fmaf(w->c[i], w->P[i], -t);
@@ -543,6 +561,7 @@ int oracle_reset(void* ctx, int B, const float* omega, const double* g_rec, cons
             Grid g = arange(0.0, cfg->transient_len, cfg->dt);
             float* yb = y + (size_t)b * N;
             memcpy(yb, theta0 + (size_t)b * N, sizeof(float) * N);
+            w.kn = kn_of(o, b);
             Stats st = {0, 0, 0, 0};
             Sink sk = {NULL, lf, lr, g.n - 1 - W, g.n - 1, g_rec + (size_t)b * cfg->n_rec * N};
             solve(o, &w, &g, yb, omega + (size_t)b * N, w.zero, &sk, &st);
@@ -588,6 +607,7 @@ int oracle_step(void* ctx, int B, const float* omega, const double* g_stim, cons
 #pragma omp for schedule(dynamic, 1)
         for (int b = 0; b < B; ++b) {
             if (rc) continue;
+            w.kn = kn_of(o, b);
             Stats st = {0, 0, 0, 0};
             double u[16];
             for (int e = 0; e < NE && e < 16; ++e) u[e] = rescale_action(cfg, action[(size_t)b * NE + e]);
@@ -669,6 +689,7 @@ int oracle_solve_rows(void* ctx, const float* omega, const float* pulse, const d
     const int N = o->N;
     Work w;
     if (work_alloc(&w, N)) return KURA_E_NOMEM;
+    w.kn = o->cfg.kn;
     Grid g;
     g.start = ts[0];
     g.delta = 0.0;
@@ -695,6 +716,7 @@ void oracle_rhs(void* ctx, const float* y, const float* omega, const float* puls
     OCtx* o = (OCtx*)ctx;
     Work w;
     if (work_alloc(&w, o->N)) return;
+    w.kn = o->cfg.kn;
     rhs(o, &w, y, omega, pulse, f);
     work_free(&w);
 }

@@ -55,6 +55,8 @@ def lib() -> ctypes.CDLL:
             getattr(L, n).argtypes = [c_void_p, c_void_p, c_int]
         L.oracle_gemm_chain.argtypes = [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int]
         L.oracle_lfp.argtypes = [c_void_p] * 5
+        L.oracle_set_gain.restype = c_int
+        L.oracle_set_gain.argtypes = [c_void_p, c_int, c_void_p]
         _lib = L
     return _lib
 
@@ -85,6 +87,10 @@ class Oracle:
         nr = max(self.cfg.n_rec, 1)
         self.g_rec = (np.ascontiguousarray(g_rec, np.float64) if g_rec is not None
                       else np.zeros((self.B, nr, self.N), np.float64))
+
+    def set_gain(self, kn):
+        self._kn = np.ascontiguousarray(kn, np.float32).reshape(-1)
+        assert lib().oracle_set_gain(self._ctx, len(self._kn), self._kn.ctypes.data) == 0
 
     def set_spectral(self, ctab, stab):
         self.ctab = np.ascontiguousarray(ctab, np.float64)

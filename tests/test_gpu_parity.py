@@ -66,7 +66,7 @@ def test_mfma_gemm_is_fmaf_chain(lib, N):
     np.testing.assert_array_equal(Y, ko.gemm_chain(X, A))
 
 
-def _run_pair(torch, name, N, B, reward, steps, act, check_every=1):
+def _run_pair(torch, name, N, B, reward, steps, act, check_every=1, gains=None):
     sim_mod = importlib.import_module("dbs-gym_amd.sim")
     cfg, alpha, omega, gs, gr, th0, ct, st, _ = make_case(name, N, B, reward=reward)
     sim = sim_mod.KuraSim(cfg, 0)
@@ -76,6 +76,9 @@ def _run_pair(torch, name, N, B, reward, steps, act, check_every=1):
     o = ko.Oracle(cfg, alpha)
     o.set_env_params(omega, gs, gr)
     o.set_spectral(ct, st)
+    if gains is not None:
+        sim.set_env_gain(gains)
+        o.set_gain(gains)
     obs_g = sim.reset(torch.from_numpy(th0)).cpu().numpy()
     obs_o = o.reset(th0)
     np.testing.assert_array_equal(obs_g, obs_o)
@@ -115,6 +118,15 @@ def _cmp_state(g, o, where):
 ])
 def test_step_parity_short(torch_gpu, name, N, reward, act):
     _run_pair(torch_gpu, name, N, 19, reward, 12, act)
+
+
+def test_step_parity_random_gain(torch_gpu):
+    """north_star 'random K': per-env coupling K ~ U(0.3, 0.8) (kura_set_env_gain)."""
+    rng = np.random.default_rng(7)
+    N, B = 512, 19
+    gains = (rng.uniform(0.3, 0.8, B) / N).astype(np.float32)
+    g, o = _run_pair(torch_gpu, "env0", N, B, "bbpow_action", 8, "rand", gains=gains)
+    np.testing.assert_array_equal(g["y"], o["y"])
 
 
 def test_phase_gate_1000_steps(torch_gpu):

@@ -19,6 +19,7 @@ class Args:
     envs = 3
     reward = "bbpow_action"
     seed = 99
+    random_k = True  # per-env K derived from the global env id, like the seeds
 
 
 def _run_shard(rank, B):
@@ -28,9 +29,10 @@ def _run_shard(rank, B):
     import bench
     a = Args()
     a.envs = B
-    cfg, alpha, omega, gs, gr, th0, ct, st = bench.build_shard(a, rank)
+    cfg, alpha, omega, gs, gr, th0, ct, st, gain = bench.build_shard(a, rank)
     o = ko.Oracle(cfg, alpha)
     o.set_env_params(omega, gs, gr)
+    o.set_gain(gain)
     o.set_spectral(ct, st)
     o.reset(th0)
     rews = []
@@ -83,9 +85,10 @@ def test_two_rank_shards_equal_single_process():
     import bench
     a = Args()
     a.envs = world * Args.envs
-    cfg, alpha, omega, gs, gr, th0, ct, st = bench.build_shard(a, 0)
+    cfg, alpha, omega, gs, gr, th0, ct, st, gain = bench.build_shard(a, 0)
     o = ko.Oracle(cfg, alpha)
     o.set_env_params(omega, gs, gr)
+    o.set_gain(gain)
     o.set_spectral(ct, st)
     o.reset(th0)
     from helpers import actions

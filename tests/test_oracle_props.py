@@ -69,3 +69,32 @@ def test_hf_dbs_reduces_beta_power():
         r_hf = o_hf.step(actions("hf", 2, 1, k))
     # rewards are -1e4*bbpow - 1e-2|u|: HF pays 0.05 for |u|=5
     assert np.mean(r_hf["reward"] + 0.05) > np.mean(r_off["reward"])
+
+
+def test_per_env_gain_matches_single_env_config():
+    """Per-env K (kura_set_env_gain / oracle_set_gain): env b of a batch with
+    gains [k0, k1] evolves exactly like a one-env run whose config kn is k_b."""
+    import copy
+    case = make_case("env0", 256, 2)
+    gains = np.array([np.float32(0.31 / 256), np.float32(0.77 / 256)], np.float32)
+    o2, th2 = _oracle(case)
+    o2.set_gain(gains)
+    o2.reset(th2)
+    singles = []
+    for b in range(2):
+        cfg1 = copy.copy(case[0])
+        cfg1.n_envs = 1
+        cfg1.kn = float(gains[b])
+        cfg_, alpha, omega, gs, gr, th0, ct, st, _ = case
+        o1 = ko.Oracle(cfg1, alpha)
+        o1.set_env_params(omega[b:b + 1], gs[b:b + 1], gr[b:b + 1])
+        o1.set_spectral(ct, st)
+        o1.reset(th0[b:b + 1])
+        singles.append(o1)
+    for k in range(3):
+        a = actions("rand", 2, 1, k)
+        o2.step(a)
+        for b in range(2):
+            singles[b].step(a[b:b + 1])
+            np.testing.assert_array_equal(o2.y[b], singles[b].y[0])
+    assert not np.array_equal(o2.y[0], o2.y[1])

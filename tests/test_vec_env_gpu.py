@@ -25,6 +25,7 @@ def _mirror(venv):
     bins = kura.spectral.beta_bins(venv.cfg.window, 0.05)
     o.set_spectral(*kura.spectral.twiddles(venv.cfg.window, bins))
     hosts = [kura.EnvHost(p) for p in venv.params]
+    o.set_gain(np.array([np.float32(p["K"] / p["num_oscillators"]) for p in venv.params], np.float32))
     return o, hosts
 
 
@@ -86,4 +87,39 @@ def test_single_env_dropin_and_reward_methods(torch_gpu):
         cfg.reward_kind = kind
         ref = ko.lib().oracle_reward(ko.ctypes.byref(cfg), x.ctypes.data, 1.5, o.ctab.ctypes.data, o.stab.ctypes.data)
         assert fn(x, [1.5]) == ref
+    env.close()
+
+
+def test_env2_drift_and_per_env_K(torch_gpu):
+    """env2 (plasticity drift, electrode moves, encapsulation at every reset)
+    with a different K per env, through two autoreset episodes."""
+    vec = importlib.import_module("dbs-gym_amd.vec_env")
+    B = 4
+    plist = []
+    for b in range(B):
+        p = kura.reference_params("env2", "train", b)
+        p["K"] = [0.35, 0.52, 0.61, 0.78][b]
+        plist.append(p)
+    env = vec.KuraVectorEnv(plist, reward_func="temp_const_action")
+    env.episode_steps = 2
+    o, hosts = _mirror(env)
+    N = env.N
+    ne, nr = env.cfg.n_elec, max(env.cfg.n_rec, 1)
+    st = dict(w=np.zeros((B, N)), gs=np.zeros((B, ne, N)), gr=np.zeros((B, nr, N)), th=np.zeros((B, N)))
+    obs, _ = env.reset()
+    _draw(o, hosts, range(B), st)
+    np.testing.assert_array_equal(obs[:, 0].cpu().numpy(), o.reset(st["th"].astype(np.float32)))
+    rng = np.random.default_rng(11)
+    for k in range(4):
+        a = rng.uniform(-1, 1, (B, ne)).astype(np.float32)
+        obs, rew, term, trunc, info = env.step(a)
+        ref = o.step(a)
+        np.testing.assert_array_equal(rew.cpu().numpy(), ref["reward"])
+        if (k + 1) % 2 == 0:
+            np.testing.assert_array_equal(info["terminal_observation"][:, 0].cpu().numpy(), ref["obs"])
+            _draw(o, hosts, range(B), st)
+            np.testing.assert_array_equal(obs[:, 0].cpu().numpy(), o.reset(st["th"].astype(np.float32)))
+        else:
+            np.testing.assert_array_equal(obs[:, 0].cpu().numpy(), ref["obs"])
+    np.testing.assert_array_equal(env.sim.get_state()["y"], o.state()["y"])
     env.close()

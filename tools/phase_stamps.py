@@ -33,9 +33,11 @@ def main():
         envs = int(os.environ.get("ENVS", "4096"))
         reward = "bbpow_action"
         seed = 7
-    cfg, alpha, omega, gs, gr, th0, ct, st = bench.build_shard(A, 0)
+        random_k = False
+    cfg, alpha, omega, gs, gr, th0, ct, st, gain = bench.build_shard(A, 0)
     sim = sim_mod.KuraSim(cfg, 0, lib_path=LIB)
     sim.set_coupling(alpha)
+    sim.set_env_gain(gain)
     sim.set_env_params(omega, gs, gr)
     sim.set_spectral(ct, st)
     sim.reset(torch.from_numpy(th0))
