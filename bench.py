@@ -97,6 +97,11 @@ def cpu_baseline(args, cfg, alpha, omega, g_stim, g_rec, theta0, ctab, stab, gai
                       f"OpenMP {nthreads} threads (one env per thread)"}
 
 
+def kernel_name(N):
+    """The step kernel instantiation libkura launches for N oscillators."""
+    return f"kura_step_kernel<{min(N, 1024) // 256}, {'true' if N > 1024 else 'false'}>"
+
+
 def pmc_traffic(N, B):
     """Bytes per launch of the step kernel from the committed rocprofv3 PMC
     passes (tools/rocprof_run.sh + tools/summarize_rocprof.py: FETCH_SIZE x2 +
@@ -110,7 +115,7 @@ def pmc_traffic(N, B):
         wl = d["bench_under_trace"]["config"]["workload"]
         if f"N={N} " not in wl or f"x {B} envs" not in wl:
             return None, None
-        k = d["kernels"][f"kura_step_kernel<{N // 256}>"]
+        k = d["kernels"][kernel_name(N)]
         return k["traffic_bytes_per_dispatch"], f"profiles/latest_rocprof.json ({d['source']}): FETCH_SIZE*2 + WRITE_SIZE"
     except (OSError, KeyError, ValueError):
         return None, None
@@ -199,7 +204,7 @@ def main():
         bytes_launch = B * bytes_env + 4 * N * N
         traffic, traffic_src = pmc_traffic(N, B)
         out = {
-            "metric": "env steps/sec (whole node), N=1024 osc x 4096 envs per GPU",
+            "metric": f"env steps/sec (whole node), N={N} osc x {B} envs per GPU",
             "value": value,
             "unit": "env-steps/s",
             "n_gpus": world,
@@ -218,7 +223,7 @@ def main():
             "roofline": {"bound": "mfma", "achieved": achieved_tf, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
                          "frac": achieved_tf / PEAK_FP32_TFLOPS, "traffic": traffic,
                          "traffic_source": traffic_src,
-                         "kernel": "kura_step_kernel<4>", "avg_kernel_ms": avg_kernel_s * 1e3,
+                         "kernel": kernel_name(N), "avg_kernel_ms": avg_kernel_s * 1e3,
                          "flop_per_launch": flop_per_launch, "useful_rhs_per_launch": useful_rhs,
                          "hbm_alg_bytes_per_launch": bytes_launch,
                          "hbm_alg_gbs": bytes_launch / avg_kernel_s / 1e9},

@@ -99,13 +99,18 @@ def reference_params(name: str = "env0", split: str = "train", idx: int = 0, **o
 
 def synthetic_params(name: str = "env0", n_osc: int = 1024, **overrides) -> dict:
     """BASELINE.json synthetic configs: the reference config scaled to N
-    oscillators on a regular grid with spacing 0.1: 16x8x8 for N=1024
-    (SURVEY.md section 8(d)), 8x8x(N/64) below, so the reference-indexed
+    oscillators on a regular grid with spacing 0.1: 16x8x8 for N=1024 and
+    32x16x16 for the N=8192 stress config,
+    16x16x8 / 16x16x16 for 2048 / 4096, 8x8x(N/64) below, so the reference-indexed
     electrode [4,3,4], recorder [1,1,1] and locus [4,4,4] stay on the grid."""
     if n_osc % 64 or n_osc < 256:
         raise ValueError("synthetic grids need n_osc >= 256 and a multiple of 64")
     d = reference_params(name, "train", **overrides)
     d["num_oscillators"] = n_osc
-    d["grid_size"] = [n_osc // 64, 8, 8] if n_osc >= 512 else [8, 8, n_osc // 64]
+    big = {2048: [16, 16, 8], 4096: [16, 16, 16], 8192: [32, 16, 16]}   # 8192: SURVEY 8(d) stress grid
+    if n_osc in big:
+        d["grid_size"] = big[n_osc]
+    else:
+        d["grid_size"] = [n_osc // 64, 8, 8] if n_osc >= 512 else [8, 8, n_osc // 64]
     d.update(overrides)
     return d

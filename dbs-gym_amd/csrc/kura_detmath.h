@@ -169,7 +169,9 @@ KDM_FN float kdm_inv_fifth_root(float xf) {
 //     32*(w*TPW + t) + c, TPW = N/256; each column lane c sums its TPW values
 //     in t order from +0, the 32 lanes combine by an xor butterfly
 //     (16,8,4,2,1: p[c] = p[c] + p[c^o]), then the 8 wave totals are added in
-//     wave order from +0.
+//     wave order from +0.  N > 1024: each part of 1024 oscillators (one
+//     workgroup of a split group) reduces that way and the part totals are
+//     added in part order from +0.
 // R64 (sums over the W-sample window: DFT bins, filtfilt mean) -- lane l
 //     (0..63) sums x[l], x[l+64], ... from +0, then an xor butterfly with
 //     offsets 32,16,8,4,2,1.

@@ -89,8 +89,17 @@ struct DevParams {
     float* R;               // [B/16][NSLOT][N][16] solver workspace: per slot, 16 envs per oscillator
     float* pulse;           // [B][N]
     double* scratch;        // [B][W + 2*padlen] * 2 (R2 filtfilt)
-    unsigned long long* stats;  // [4]: max rhs, steps, rejected, flags
-    unsigned long long* stamps; // [NWAVES][8] phase cycle counters (KURA_STAMPS builds only)
+    unsigned long long* stats;  // [KURA_NSTATS] (kura.h)
+    unsigned long long* stamps; // [NWAVES][KURA_NSTAMP] phase cycle counters (KURA_STAMPS builds only)
+    // split groups (N > 1024): npart workgroups share an env group, each owns
+    // 1024 oscillators; they exchange sin/cos images and partial sums through
+    // global memory with agent-scope release/acquire (group_barrier).
+    int npart;              // workgroups per env group (1 when N <= 1024)
+    int npairs;             // env groups x npart
+    float* xg;              // [group][2][npart][xs_floats(1024)] sin/cos images
+    float* xred;            // [group][2][npart][RC][16] f32 partial sums
+    double* xredd;          // [group][2][npart][RC][16] f64 partial sums
+    unsigned* gcnt;         // [group][16] arrival counters, zeroed before every launch
 };
 
 // Diagnostic phase timers (compile with -DKURA_STAMPS): per wave, cycles
@@ -123,6 +132,12 @@ __shared__ double s_smp_r[E_WG][KURA_S_MAX + 2];
 // R64-layout stage-input writes bank-conflict free.
 #define XS_HALF 132
 #define XS_BLOCK 264
+// split groups (N > 1024)
+#define XL_NL 1024                       // oscillators per part
+#define XL_IMG (XL_NL / 8 * XS_BLOCK)    // floats of one part's LDS/global image
+#define XL_KC 512                        // oscillators per streamed GEMM chunk
+#define XL_CIMG (XL_KC / 8 * XS_BLOCK)   // floats of one chunk image
+#define XL_SPIN_MAX (1u << 25)
 __host__ __device__ constexpr int xs_floats(int N) { return (N / 8) * XS_BLOCK; }
 __device__ __forceinline__ int xs_idx(int row, int k) {
     return (k >> 3) * XS_BLOCK + (k & 1) * XS_HALF + (row << 2) + ((k >> 1) & 3);
@@ -259,6 +274,93 @@ __device__ __forceinline__ void lds_barrier() {
     asm volatile("" ::: "memory");
 }
 
+// Split-group GEMM (N > 1024): the same MFMA chain over all N oscillators
+// (k ascending, so P/Q are bit-identical to coupling_gemm's), with the
+// 32 x N sin/cos operand streamed from the group's global image (xg) through
+// two LDS chunk buffers of XL_KC oscillators, and this workgroup's 1024 output
+// columns (col0 ..) of alpha.
+template <int TPW>
+__device__ __forceinline__ void coupling_gemm_xl(const float* __restrict__ xg, const float* __restrict__ alpha_sw,
+                                                 float* Xs, int NG, int col0, floatx16 (&acc)[TPW]) {
+    const int NK8 = NG / 8;
+    const int TSTRIDE = NK8 * 64;  // floatx4 per column tile
+    const int nchunk = NG / XL_KC;
+    int lane;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+#pragma unroll
+    for (int t = 0; t < TPW; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[t][r] = 0.0f;
+    const float* au = uniform_ptr(alpha_sw);
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(au + ((size_t)(col0 / 32) + wave * TPW) * TSTRIDE * 4), 0, TPW * TSTRIDE * 16, 0x00020000);
+    auto ld = [&](int t, int k) -> floatx4 {
+        return __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(rs, (lane + k * 64) * 16,
+                                                                                 t * TSTRIDE * 16, 0));
+    };
+    // chunk 0 -> LDS buffer 0
+    constexpr int C4 = XL_CIMG / 4;               // floatx4 per chunk image
+    constexpr int CPT = (C4 + NTHREADS - 1) / NTHREADS;
+    const floatx4* xg4 = (const floatx4*)xg;
+    floatx4* xs4w = (floatx4*)Xs;
+    for (int k = threadIdx.x; k < C4; k += NTHREADS) xs4w[k] = xg4[k];
+    lds_barrier();
+    floatx4 b0[TPW], b1[TPW];
+#pragma unroll
+    for (int t = 0; t < TPW; ++t) {
+        b0[t] = ld(t, 0);
+        b1[t] = ld(t, 1);
+    }
+#pragma unroll 1
+    for (int c = 0; c < nchunk; ++c) {
+        // stage the next chunk in registers while this one multiplies
+        floatx4 nx[CPT];
+        const bool more = c + 1 < nchunk;
+#pragma unroll
+        for (int u = 0; u < CPT; ++u) {
+            const int k = threadIdx.x + u * NTHREADS;
+            if (more && k < C4) nx[u] = xg4[(size_t)(c + 1) * C4 + k];
+        }
+        const floatx4* xs4 = reinterpret_cast<const floatx4*>(Xs + (c & 1) * XL_CIMG + (lane >> 5) * XS_HALF +
+                                                              (lane & 31) * 4);
+        const int kg0 = c * (XL_KC / 8);
+#pragma unroll 1
+        for (int kb = 0; kb < XL_KC / 8; kb += 2) {
+            floatx4 a = xs4[kb * (XS_BLOCK / 4)];
+#pragma unroll
+            for (int s = 0; s < 4; ++s)
+#pragma unroll
+                for (int t = 0; t < TPW; ++t)
+                    acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s], b0[t][s], acc[t], 0, 0, 0);
+            const int k2 = kg0 + kb + 2 < NK8 ? kg0 + kb + 2 : NK8 - 1;
+#pragma unroll
+            for (int t = 0; t < TPW; ++t) b0[t] = ld(t, k2);
+            __builtin_amdgcn_sched_barrier(0);
+            a = xs4[(kb + 1) * (XS_BLOCK / 4)];
+#pragma unroll
+            for (int s = 0; s < 4; ++s)
+#pragma unroll
+                for (int t = 0; t < TPW; ++t)
+                    acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s], b1[t][s], acc[t], 0, 0, 0);
+            const int k3 = kg0 + kb + 3 < NK8 ? kg0 + kb + 3 : NK8 - 1;
+#pragma unroll
+            for (int t = 0; t < TPW; ++t) b1[t] = ld(t, k3);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        if (more) {  // the other buffer was last read in chunk c-1, before the previous barrier
+            floatx4* dst = (floatx4*)(Xs + ((c + 1) & 1) * XL_CIMG);
+#pragma unroll
+            for (int u = 0; u < CPT; ++u) {
+                const int k = threadIdx.x + u * NTHREADS;
+                if (k < C4) dst[k] = nx[u];
+            }
+        }
+        lds_barrier();
+    }
+}
+
+
 // Per-env solver control.  One slot per local env lives in LDS; thread e
 // (e < 16) owns slot e's scalar decisions, every lane reads it.
 struct CtlE {
@@ -358,9 +460,11 @@ __device__ __forceinline__ void store8(const Slot& w, int slot, int t, const flo
 // f = fmaf(kn, fmaf(c, P, -(s*Q)), omega) + pulse  ->  slot F0 + stage
 // (omega and pulse come from their records, SL_W / SL_P, written at the
 // start of the solve; all TPW tiles' loads are issued before the first use)
-template <int TPW>
+// (split groups read this part's sin/cos from its published global image)
+template <int TPW, bool XL>
 __device__ __forceinline__ void coupling_epilogue(const DevParams& p, const Slot& ws, const float* __restrict__ Xs,
-                                                  const floatx16 (&acc)[TPW], int stage, bool pulse_on) {
+                                                  const float* __restrict__ xown, const floatx16 (&acc)[TPW],
+                                                  int stage, bool pulse_on) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     float w[TPW][8], u[TPW][8];
 #pragma unroll
@@ -384,7 +488,14 @@ __device__ __forceinline__ void coupling_epilogue(const DevParams& p, const Slot
         for (int q = 0; q < 8; ++q) {
             const int e = mfma_env(q, lane);
             const float P = acc[t][q], Q = acc[t][q + 8];
-            const float sn = Xs[xs_idx(e, i)], cs = Xs[xs_idx(16 + e, i)];
+            float sn, cs;
+            if constexpr (XL) {
+                sn = xown[xs_idx(e, i)];
+                cs = xown[xs_idx(16 + e, i)];
+            } else {
+                sn = Xs[xs_idx(e, i)];
+                cs = Xs[xs_idx(16 + e, i)];
+            }
             const float tq = sn * Q;
             const float coup = __builtin_fmaf(cs, P, -tq);
             f[q] = __builtin_fmaf(knq[q], coup, w[t][q]) + u[t][q];
@@ -497,12 +608,101 @@ __device__ __forceinline__ double rm_total_d(int e, int k) {
     return tot;
 }
 
+// ---- split groups (N > 1024) ---------------------------------------------
+// A workgroup's share of one env group.  For N <= 1024 there is one part
+// (npart = 1, col0 = 0) and nothing is exchanged.
+struct Part {
+    int ng;       // oscillators per env (N)
+    int col0;     // first oscillator (global column) owned by this workgroup
+    int part;     // 0 .. npart-1
+    int npart;
+    int group;    // envs [16 group, 16 group + 16)
+    int pair;     // group * npart + part: index of this workgroup's records
+    unsigned ep;  // group exchanges done so far (identical in every part)
+    int xs_n;     // sin/cos images published so far (selects the image buffer)
+};
+
+
+typedef __attribute__((address_space(1))) unsigned gu32;
+
+// Arrive at / wait for the group's barrier number ep+1 (Guideline 16 of the
+// CDNA guide: agent-scope release by every storing thread, one agent-scope
+// atomic arrival, a bounded relaxed poll, one agent-scope acquire that drops
+// this CU's stale L1 lines, then the workgroup barrier).  A poll that never
+// completes (a part not resident) gives up after ~1 s and raises stats flag
+// bit 4 instead of hanging the GPU.
+__device__ __noinline__ void group_barrier(const DevParams& p, Part& pt) {
+    __threadfence();
+    __syncthreads();
+    pt.ep += 1;
+    if (threadIdx.x == 0) {
+        gu32* cnt = (gu32*)uniform_ptr(p.gcnt + (size_t)pt.group * 16);
+        __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned target = pt.ep * (unsigned)pt.npart;
+        unsigned spins = 0;
+        while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+            __builtin_amdgcn_s_sleep(2);
+            // after one timeout every later barrier of the launch gives up at once
+            if (++spins > XL_SPIN_MAX ||
+                (__hip_atomic_load(&p.stats[3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 16ull)) {
+                atomicOr(&p.stats[3], 16ull);
+                break;
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    }
+    __syncthreads();
+}
+
+// Group-wide totals of per-env partial sums: thread e (< 16) passes its
+// part's values v[k] (k < nk); on return it holds 0 + part_0 + part_1 + ...
+// (part order) -- the RM order extended over parts (oracle_rm_*).
+template <int NK>
+__device__ __forceinline__ void group_sum(const DevParams& p, Part& pt, float (&vf)[NK], double (&vd)[NK], int nk,
+                                          bool with_d) {
+    const int tid = threadIdx.x;
+    const size_t base = ((size_t)pt.group * 2 + (pt.ep & 1)) * pt.npart * (RC * E_WG);
+    float* xr = p.xred + base;
+    double* xd = p.xredd + base;
+    if (tid < E_WG)
+        for (int k = 0; k < nk; ++k) {
+            xr[(pt.part * RC + k) * E_WG + tid] = vf[k];
+            if (with_d) xd[(pt.part * RC + k) * E_WG + tid] = vd[k];
+        }
+    group_barrier(p, pt);
+    if (tid < E_WG)
+        for (int k = 0; k < nk; ++k) {
+            float a = 0.0f;
+            double b = 0.0;
+            for (int q = 0; q < pt.npart; ++q) {
+                a = a + xr[(q * RC + k) * E_WG + tid];
+                if (with_d) b = b + xd[(q * RC + k) * E_WG + tid];
+            }
+            vf[k] = a;
+            vd[k] = b;
+        }
+}
+
+// Publish this part's sin/cos image (LDS, XL_IMG floats) into the group's
+// image buffer and wait until every part has published its own.
+__device__ __forceinline__ const float* group_publish_x(const DevParams& p, Part& pt, const float* Xs) {
+    const size_t img = ((size_t)pt.group * 2 + (pt.xs_n & 1)) * pt.npart * XL_IMG;
+    floatx4* dst = (floatx4*)(p.xg + img + (size_t)pt.part * XL_IMG);
+    const floatx4* src = (const floatx4*)Xs;
+    for (int k = threadIdx.x; k < XL_IMG / 4; k += NTHREADS) dst[k] = src[k];
+    group_barrier(p, pt);
+    pt.xs_n += 1;
+    return p.xg + img;
+}
+
 // After the 7th stage: error norm, accept/reject, dense-output saves with
 // LFP, FSAL -- for all 16 envs, every wave on its own columns.
-template <int TPW>
-__device__ __forceinline__ void post_step(const DevParams& p, const Slot& ws, int env_base, bool to_ring STAMP_PARAMS) {
+template <int TPW, bool XL>
+__device__ __forceinline__ void post_step(const DevParams& p, const Slot& ws, int env_base, bool to_ring, Part& pt
+                                          STAMP_PARAMS) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, tid = threadIdx.x;
-    constexpr int N = TPW * 256;
+    const int NG = XL ? pt.ng : TPW * 256;   // oscillators per env
+    const int col0 = XL ? pt.col0 : 0;       // this workgroup's first oscillator
     float h[8];
 #pragma unroll
     for (int q = 0; q < 8; ++q) h[q] = s_ctl[mfma_env(q, lane)].h;
@@ -554,13 +754,18 @@ __device__ __forceinline__ void post_step(const DevParams& p, const Slot& ws, in
     rm_publish(part, 0);
     STAMP(5);
     lds_barrier();
+    float etot[1] = {tid < E_WG ? rm_total(tid, 0) : 0.0f};
+    if constexpr (XL) {
+        double dummy[1] = {0.0};
+        group_sum<1>(p, pt, etot, dummy, 1, false);
+    }
     // (2) thread e: accept/reject, step-size update (diffrax PIDController)
     if (tid < E_WG) {
         CtlE& c = s_ctl[tid];
         c.nsave = 0;
         c.keep = 0;
         if (c.active) {
-            const float mean = rm_total(tid, 0) / (float)N;
+            const float mean = etot[0] / (float)NG;
             const float err = sqrtf(mean);
             const bool keep = err < 1.0f;
             float fac = 0.9f * kdm_inv_fifth_root(err);
@@ -646,7 +851,7 @@ __device__ __forceinline__ void post_step(const DevParams& p, const Slot& ws, in
                 for (int q = 0; q < 8; ++q) {
                     int env = env_base + mfma_env(q, lane);
                     env = env < p.B ? env : p.B - 1;
-                    G[q] = p.g_rec[(size_t)env * N + i];
+                    G[q] = p.g_rec[(size_t)env * NG + col0 + i];
                 }
             }
 #pragma unroll
@@ -667,7 +872,7 @@ __device__ __forceinline__ void post_step(const DevParams& p, const Slot& ws, in
                         if (gauss) pg[k][q] = pg[k][q] + (double)cr * G[q];
                     }
                     const int env = env_base + mfma_env(q, lane);
-                    if ((f & 4) && env < p.B) p.y[(size_t)env * N + i] = v;
+                    if ((f & 4) && env < p.B) p.y[(size_t)env * NG + col0 + i] = v;
                 }
         }
         // identical in every wave: each wave holds all 16 envs
@@ -681,16 +886,30 @@ __device__ __forceinline__ void post_step(const DevParams& p, const Slot& ws, in
         }
         (void)anyw;
         lds_barrier();
+        float ltot[RC];
+        double ltot_d[RC];
+#pragma unroll
+        for (int k = 0; k < RC; ++k) {
+            ltot[k] = 0.0f;
+            ltot_d[k] = 0.0;
+            if (tid < E_WG && (s_rflag[tid][k] & 2)) {
+                ltot[k] = rm_total(tid, k);
+                if (gauss) ltot_d[k] = rm_total_d(tid, k);
+            }
+        }
+        if constexpr (XL) {
+            if (__builtin_amdgcn_readfirstlane(anyw) & 02222) group_sum<RC>(p, pt, ltot, ltot_d, RC, gauss);
+        }
         if (tid < E_WG) {
             const CtlE& c = s_ctl[tid];
             for (int k = 0; k < RC; ++k) {
                 if (!(s_rflag[tid][k] & 2)) continue;
                 const int si = c.si + r0 + k;
-                const float ln = rm_total(tid, k) / (float)N;
-                const double lr = gauss ? 0.0 + rm_total_d(tid, k) / (double)N : (double)ln;
+                const float ln = ltot[k] / (float)NG;
+                const double lr = gauss ? 0.0 + ltot_d[k] / (double)NG : (double)ln;
                 const int pos = si - c.lfp_from + c.pos0;
                 if (to_ring) {
-                    p.ring[(size_t)(env_base + tid) * p.W + pos] = lr;
+                    if (!XL || pt.part == 0) p.ring[(size_t)(env_base + tid) * p.W + pos] = lr;
                 } else {
                     s_smp_n[tid][pos] = ln;
                     s_smp_r[tid][pos] = lr;
@@ -745,17 +964,20 @@ __device__ __forceinline__ void post_step(const DevParams& p, const Slot& ws, in
 
 // One diffeqsolve for the workgroup's 16 envs.  s_ctl must be initialised
 // (ctl_begin) and visible before the call.
-template <int TPW>
+template <int TPW, bool XL>
 __device__ void solve_wg(const DevParams& p, float* Xs, int env_base, bool to_ring, bool pulse_on,
-                         long long* rhs_count) {
+                         long long* rhs_count, Part& pt) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, tid = threadIdx.x;
     const int hq = lane >> 5;
-    constexpr int N = TPW * 256;
+    constexpr int N = TPW * 256;            // oscillators owned by this workgroup
+    const int NG = XL ? pt.ng : N;          // oscillators per env
+    const int col0 = XL ? pt.col0 : 0;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const Slot ws{__builtin_amdgcn_make_buffer_rsrc((void*)uniform_ptr(p.R + (size_t)blockIdx.x * NSLOT * N * 16), 0,
+    const int pair = __builtin_amdgcn_readfirstlane(pt.pair);
+    const Slot ws{__builtin_amdgcn_make_buffer_rsrc((void*)uniform_ptr(p.R + (size_t)pair * NSLOT * N * 16), 0,
                                                     NSLOT * N * 16 * 4, 0x00020000),
                   N, wv * TPW, (lane & 31) * 64 + hq * 16,
-                  (gfloat*)uniform_ptr(p.R + (size_t)blockIdx.x * NSLOT * N * 16)};
+                  (gfloat*)uniform_ptr(p.R + (size_t)pair * NSLOT * N * 16)};
     // records y0 <- state y, omega, pulse (0 while stimulation is OFF, env.py:434)
 #pragma unroll 1
     for (int t = 0; t < TPW; ++t) {
@@ -766,7 +988,7 @@ __device__ void solve_wg(const DevParams& p, float* Xs, int env_base, bool to_ri
             int env = env_base + mfma_env(q, lane);
             const bool ok = env < p.B;
             env = ok ? env : p.B - 1;  // padded slots: any valid address
-            const size_t o = (size_t)env * N + i;
+            const size_t o = (size_t)env * NG + col0 + i;
             v[q] = ok ? p.y[o] : 0.0f;
             w[q] = p.omega[o];
             u[q] = pulse_on ? p.pulse[o] : 0.0f;
@@ -789,9 +1011,16 @@ __device__ void solve_wg(const DevParams& p, float* Xs, int env_base, bool to_ri
         STAMP(0);
         lds_barrier();
         STAMP(1);
-        coupling_gemm<TPW>(Xs, p.alpha_sw, acc);
+        const float* xown = nullptr;
+        if constexpr (XL) {
+            const float* xgrp = group_publish_x(p, pt, Xs);   // all parts' images of this stage
+            xown = xgrp + (size_t)pt.part * XL_IMG;
+            coupling_gemm_xl<TPW>(xgrp, p.alpha_sw, Xs, NG, col0, acc);
+        } else {
+            coupling_gemm<TPW>(Xs, p.alpha_sw, acc);
+        }
         STAMP(2);
-        coupling_epilogue<TPW>(p, ws, Xs, acc, s, pulse_on);
+        coupling_epilogue<TPW, XL>(p, ws, Xs, xown, acc, s, pulse_on);
         STAMP(3);
         lds_barrier();
         STAMP(4);
@@ -801,7 +1030,7 @@ __device__ void solve_wg(const DevParams& p, float* Xs, int env_base, bool to_ri
             continue;
         }
         if (s == 6) {
-            post_step<TPW>(p, ws, env_base, to_ring STAMP_ARGS);
+            post_step<TPW, XL>(p, ws, env_base, to_ring, pt STAMP_ARGS);
             STAMP(10);
         }
         if (tid == 0) {
@@ -965,16 +1194,34 @@ __device__ double reward_of(const DevParams& p, const double (&x)[WPL], double u
 #define WPL_MAX 40  // ceil(W/64) upper bound supported (W <= 2560)
 
 // ------------------------------------------------------------ step kernel --
-template <int TPW>
-__global__ __launch_bounds__(NTHREADS) void kura_step_kernel(DevParams p, const float* __restrict__ action,
-                                                             float* __restrict__ obs, double* __restrict__ reward,
-                                                             uint8_t* __restrict__ done, float* __restrict__ lfp_true,
-                                                             double* __restrict__ lfp_rec, int* __restrict__ nsamp) {
-    extern __shared__ float Xs[];  // xs_floats(N)
+// Work item of a launch: (env group, part).  For N <= 1024 one workgroup per
+// group; split groups loop persistently over pairs with a grid that is a
+// multiple of npart and at most one workgroup per CU, so every part of a
+// group is resident at the same time.
+__device__ __forceinline__ Part make_part(const DevParams& p, int pair) {
+    Part pt;
+    pt.npart = p.npart;
+    pt.group = pair / p.npart;
+    pt.part = pair - pt.group * p.npart;
+    pt.ng = p.N;
+    pt.col0 = pt.part * XL_NL;
+    pt.pair = pair;
+    pt.ep = 0;
+    pt.xs_n = 0;
+    return pt;
+}
+
+template <int TPW, bool XL>
+__device__ __forceinline__ void step_pair(const DevParams& p, Part& pt, float* Xs, const float* __restrict__ action,
+                                          float* __restrict__ obs, double* __restrict__ reward,
+                                          uint8_t* __restrict__ done, float* __restrict__ lfp_true,
+                                          double* __restrict__ lfp_rec, int* __restrict__ nsamp) {
     __shared__ int s_nI[E_WG], s_nII[E_WG];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, tid = threadIdx.x;
     const int N = p.N;
-    const int env_base = blockIdx.x * E_WG;
+    const int env_base = pt.group * E_WG;
+    const int c0 = XL ? pt.col0 : 0, c1 = XL ? pt.col0 + XL_NL : N;   // oscillators of this workgroup
+    __syncthreads();  // previous pair's LDS readers
     ctl_clear();
     // ---- thread e: rescale_action (env.py:389-393), ON grid (env.py:426-428)
     if (tid < E_WG) {
@@ -1005,7 +1252,7 @@ __global__ __launch_bounds__(NTHREADS) void kura_step_kernel(DevParams p, const 
         const int env = env_base + e;
         if (env >= p.B) continue;
         const int ne = p.n_elec < 4 ? p.n_elec : 4;
-        for (int i = lane; i < N; i += 64) {
+        for (int i = c0 + lane; i < c1; i += 64) {
             double pacc = 0.0;
             for (int k = 0; k < ne; ++k) pacc = pacc + p.g_stim[((size_t)env * p.n_elec + k) * N + i] * s_u[e][k];
             p.pulse[(size_t)env * N + i] = (float)pacc;
@@ -1013,7 +1260,7 @@ __global__ __launch_bounds__(NTHREADS) void kura_step_kernel(DevParams p, const 
     }
     __syncthreads();
     long long rhs = 0;
-    solve_wg<TPW>(p, Xs, env_base, false, true, &rhs);
+    solve_wg<TPW, XL>(p, Xs, env_base, false, true, &rhs, pt);
     __syncthreads();  // global stores of the solve (y) before the OFF setup
     // ---- stimulation OFF (env.py:433-441)
     if (tid < E_WG) {
@@ -1036,12 +1283,13 @@ __global__ __launch_bounds__(NTHREADS) void kura_step_kernel(DevParams p, const 
         }
     }
     __syncthreads();
-    solve_wg<TPW>(p, Xs, env_base, false, false, &rhs);
+    solve_wg<TPW, XL>(p, Xs, env_base, false, false, &rhs, pt);
     __syncthreads();
     // ---- window, reward, outputs (env.py:443-454): wave w owns envs 2w, 2w+1
+    // (split groups: part 0; every part holds the same samples)
     constexpr int WPL = WPL_MAX;
 #pragma unroll 1
-    for (int ee = 0; ee < ENVS_PER_WAVE; ++ee) {
+    for (int ee = 0; ee < ((!XL || pt.part == 0) ? ENVS_PER_WAVE : 0); ++ee) {
         const int e = wave * ENVS_PER_WAVE + ee;
         const int env = env_base + e;
         if (env >= p.B) continue;
@@ -1094,18 +1342,36 @@ __global__ __launch_bounds__(NTHREADS) void kura_step_kernel(DevParams p, const 
             if (lfp_rec) lfp_rec[(size_t)env * KURA_S_MAX + lane] = lane < S ? s_smp_r[e][lane] : 0.0;
         }
     }
-    flush_stats(p, rhs, env_base);
+    if (!XL || pt.part == 0) flush_stats(p, rhs, env_base);
+}
+
+template <int TPW, bool XL>
+__global__ __launch_bounds__(NTHREADS) void kura_step_kernel(DevParams p, const float* __restrict__ action,
+                                                             float* __restrict__ obs, double* __restrict__ reward,
+                                                             uint8_t* __restrict__ done, float* __restrict__ lfp_true,
+                                                             double* __restrict__ lfp_rec, int* __restrict__ nsamp) {
+    extern __shared__ float Xs[];  // xs_floats(min(N, 1024))
+    if constexpr (XL) {
+#pragma unroll 1
+        for (int pair = blockIdx.x; pair < p.npairs; pair += gridDim.x) {
+            Part pt = make_part(p, pair);
+            step_pair<TPW, XL>(p, pt, Xs, action, obs, reward, done, lfp_true, lfp_rec, nsamp);
+        }
+    } else {
+        Part pt = make_part(p, blockIdx.x);
+        step_pair<TPW, XL>(p, pt, Xs, action, obs, reward, done, lfp_true, lfp_rec, nsamp);
+    }
 }
 
 // ----------------------------------------------------------- reset kernel --
-template <int TPW>
-__global__ __launch_bounds__(NTHREADS) void kura_reset_kernel(DevParams p, const uint8_t* __restrict__ mask,
-                                                              const float* __restrict__ theta0,
-                                                              float* __restrict__ obs) {
-    extern __shared__ float Xs[];
+template <int TPW, bool XL>
+__device__ __forceinline__ void reset_pair(const DevParams& p, Part& pt, float* Xs, const uint8_t* __restrict__ mask,
+                                           const float* __restrict__ theta0, float* __restrict__ obs) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, tid = threadIdx.x;
     const int N = p.N, W = p.W;
-    const int env_base = blockIdx.x * E_WG;
+    const int env_base = pt.group * E_WG;
+    const int c0 = XL ? pt.col0 : 0, c1 = XL ? pt.col0 + XL_NL : N;
+    __syncthreads();
     ctl_clear();
     if (tid < E_WG) {
         const int env = env_base + tid;
@@ -1119,14 +1385,14 @@ __global__ __launch_bounds__(NTHREADS) void kura_reset_kernel(DevParams p, const
     for (int ee = 0; ee < ENVS_PER_WAVE; ++ee) {
         const int env = env_base + wave * ENVS_PER_WAVE + ee;
         if (env >= p.B || (mask && !mask[env])) continue;
-        for (int i = lane; i < N; i += 64) p.y[(size_t)env * N + i] = theta0[(size_t)env * N + i];
+        for (int i = c0 + lane; i < c1; i += 64) p.y[(size_t)env * N + i] = theta0[(size_t)env * N + i];
     }
     __syncthreads();
     long long rhs = 0;
-    solve_wg<TPW>(p, Xs, env_base, true, false, &rhs);
+    solve_wg<TPW, XL>(p, Xs, env_base, true, false, &rhs, pt);
     __syncthreads();  // ring rows written by thread e are read by every lane below
 #pragma unroll 1
-    for (int ee = 0; ee < ENVS_PER_WAVE; ++ee) {
+    for (int ee = 0; ee < ((!XL || pt.part == 0) ? ENVS_PER_WAVE : 0); ++ee) {
         const int e = wave * ENVS_PER_WAVE + ee;
         const int env = env_base + e;
         if (env >= p.B || (mask && !mask[env])) continue;
@@ -1138,7 +1404,24 @@ __global__ __launch_bounds__(NTHREADS) void kura_reset_kernel(DevParams p, const
         if (obs)
             for (int i = lane; i < W; i += 64) obs[(size_t)env * W + i] = (float)p.ring[(size_t)env * W + i];
     }
-    flush_stats(p, rhs, env_base);
+    if (!XL || pt.part == 0) flush_stats(p, rhs, env_base);
+}
+
+template <int TPW, bool XL>
+__global__ __launch_bounds__(NTHREADS) void kura_reset_kernel(DevParams p, const uint8_t* __restrict__ mask,
+                                                              const float* __restrict__ theta0,
+                                                              float* __restrict__ obs) {
+    extern __shared__ float Xs[];
+    if constexpr (XL) {
+#pragma unroll 1
+        for (int pair = blockIdx.x; pair < p.npairs; pair += gridDim.x) {
+            Part pt = make_part(p, pair);
+            reset_pair<TPW, XL>(p, pt, Xs, mask, theta0, obs);
+        }
+    } else {
+        Part pt = make_part(p, blockIdx.x);
+        reset_pair<TPW, XL>(p, pt, Xs, mask, theta0, obs);
+    }
 }
 
 // ------------------------------------------------------ standalone reward --

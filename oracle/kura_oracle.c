@@ -104,7 +104,7 @@ double oracle_r64_f64(const double* x, int n) {
  * (TPW = N/256 column tiles, c = 0..31); per column lane c the TPW values are
  * summed in t order, the 32 lanes combine by an xor butterfly (16,8,4,2,1),
  * and the 8 wave totals are added in wave order from +0. */
-float oracle_rm_f32(const float* x, int n) {
+static float rm_part_f32(const float* x, int n) {
     const int tpw = n / 256;
     float tot = 0.0f;
     for (int w = 0; w < 8; ++w) {
@@ -123,7 +123,7 @@ float oracle_rm_f32(const float* x, int n) {
     return tot;
 }
 
-double oracle_rm_f64(const double* x, int n) {
+static double rm_part_f64(const double* x, int n) {
     const int tpw = n / 256;
     double tot = 0.0;
     for (int w = 0; w < 8; ++w) {
@@ -139,6 +139,23 @@ double oracle_rm_f64(const double* x, int n) {
         }
         tot = tot + p[0];
     }
+    return tot;
+}
+
+/* N > 1024: the kernel splits the oscillators into parts of 1024 (one
+ * workgroup each); each part reduces in the order above and the part totals
+ * are added in part order from +0. */
+float oracle_rm_f32(const float* x, int n) {
+    if (n <= 1024) return rm_part_f32(x, n);
+    float tot = 0.0f;
+    for (int q = 0; q < n / 1024; ++q) tot = tot + rm_part_f32(x + (size_t)q * 1024, 1024);
+    return tot;
+}
+
+double oracle_rm_f64(const double* x, int n) {
+    if (n <= 1024) return rm_part_f64(x, n);
+    double tot = 0.0;
+    for (int q = 0; q < n / 1024; ++q) tot = tot + rm_part_f64(x + (size_t)q * 1024, 1024);
     return tot;
 }
 

@@ -1,0 +1,73 @@
+"""Split env groups (N > 1024): one env group of 16 spread over N/1024
+workgroups that exchange sin/cos images and partial sums through global
+memory.  GPU results must stay bit-identical to the oracle (whose RM order
+adds the 1024-oscillator part totals in part order)."""
+import importlib
+import os
+
+import numpy as np
+import pytest
+
+from helpers import actions, ko, make_case
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def torch_gpu():
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch
+
+
+def _pair(torch, N, B, steps, reward="bbpow_action", name="env0", gains=None):
+    sim_mod = importlib.import_module("dbs-gym_amd.sim")
+    cfg, alpha, omega, gs, gr, th0, ct, st, _ = make_case(name, N, B, reward=reward)
+    sim = sim_mod.KuraSim(cfg, 0)
+    sim.set_coupling(alpha)
+    sim.set_env_params(omega, gs, gr)
+    sim.set_spectral(ct, st)
+    o = ko.Oracle(cfg, alpha)
+    o.set_env_params(omega, gs, gr)
+    o.set_spectral(ct, st)
+    if gains is not None:
+        sim.set_env_gain(gains)
+        o.set_gain(gains)
+    obs_g = sim.reset(torch.from_numpy(th0)).cpu().numpy()
+    np.testing.assert_array_equal(obs_g, o.reset(th0))
+    assert not (sim.stats()[3] & 16), "group barrier timed out"
+    for k in range(steps):
+        a = actions("rand", B, cfg.n_elec, k)
+        sim.step(torch.from_numpy(a))
+        ref = o.step(a)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(sim.obs.cpu().numpy(), ref["obs"])
+        np.testing.assert_array_equal(sim.reward.cpu().numpy(), ref["reward"])
+        np.testing.assert_array_equal(sim.lfp_rec.cpu().numpy(), ref["lfp_rec"])
+    g = sim.get_state()
+    np.testing.assert_array_equal(g["y"], o.state()["y"])
+    np.testing.assert_array_equal(g["t"], o.state()["t"])
+    assert not (sim.stats()[3] & 16)
+    sim.close()
+
+
+def test_split_n2048_two_parts(torch_gpu):
+    _pair(torch_gpu, 2048, 19, 4)
+
+
+def test_split_n4096_env1_random_gain(torch_gpu):
+    rng = np.random.default_rng(3)
+    _pair(torch_gpu, 4096, 16, 2, reward="temp_const_action", name="env1",
+          gains=(rng.uniform(0.3, 0.8, 16) / 4096).astype(np.float32))
+
+
+def test_split_persistent_pair_loop(torch_gpu, monkeypatch):
+    """Grid capped below the number of (group, part) pairs: workgroups loop."""
+    monkeypatch.setenv("KURA_XL_MAX_GRID", "4")
+    _pair(torch_gpu, 2048, 40, 2)          # 3 groups x 2 parts on a grid of 4
+
+
+def test_split_n8192_stress_config(torch_gpu):
+    """BASELINE.json configs[4]: N=8192 all-to-all coupling (8 parts per group)."""
+    _pair(torch_gpu, 8192, 16, 2)
