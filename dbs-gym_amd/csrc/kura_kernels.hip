@@ -836,8 +836,14 @@ __device__ __forceinline__ void post_step(const DevParams& p, const Slot& ws, in
                 pn[k][q] = 0.0f;
                 pg[k][q] = 0.0;
             }
+        // identical in every wave: each wave holds all 16 envs
+        const int anyw = __any(anyl) ? (anyl | __shfl_xor(anyl, 32, 64)) : 0;
+        // rows that feed neither an LFP sample nor the final state (the first
+        // 3999 - W saves of the reset transient) need no evaluation at all
+        const int flor = fl[0] | fl[1] | fl[2] | fl[3] | fl[4] | fl[5] | fl[6] | fl[7];
+        const bool eval_rows = __any(flor & 06666);  // LFP or final-row bits of any round
 #pragma unroll 1
-        for (int t = 0; t < TPW; ++t) {
+        for (int t = 0; t < (eval_rows ? TPW : 0); ++t) {
             const int i = 32 * (wave * TPW + t) + (lane & 31);
             float ca[8], cb[8], cc[8], f0[8], y0[8];
             double G[8];
@@ -875,8 +881,6 @@ __device__ __forceinline__ void post_step(const DevParams& p, const Slot& ws, in
                     if ((f & 4) && env < p.B) p.y[(size_t)env * NG + col0 + i] = v;
                 }
         }
-        // identical in every wave: each wave holds all 16 envs
-        const int anyw = __any(anyl) ? (anyl | __shfl_xor(anyl, 32, 64)) : 0;
 #pragma unroll
         for (int k = 0; k < RC; ++k) {
             if (__any((anyl >> (3 * k)) & 2)) {
