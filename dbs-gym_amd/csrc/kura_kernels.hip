@@ -282,6 +282,11 @@ __device__ __forceinline__ void lds_barrier() {
 template <int TPW>
 __device__ __forceinline__ void coupling_gemm_xl(const float* __restrict__ xg, const float* __restrict__ alpha_sw,
                                                  float* Xs, int NG, int col0, floatx16 (&acc)[TPW]) {
+    // (xg, NG, col0 arrive through the VGPR-passed Part of the non-inlined
+    // solver; they are wave-uniform, readfirstlane makes that provable)
+    NG = __builtin_amdgcn_readfirstlane(NG);  // all addressing below must be provably uniform
+    col0 = __builtin_amdgcn_readfirstlane(col0);
+    xg = uniform_ptr(xg);
     const int NK8 = NG / 8;
     const int TSTRIDE = NK8 * 64;  // floatx4 per column tile
     const int nchunk = NG / XL_KC;
@@ -302,7 +307,7 @@ __device__ __forceinline__ void coupling_gemm_xl(const float* __restrict__ xg, c
     // chunk 0 -> LDS buffer 0
     constexpr int C4 = XL_CIMG / 4;               // floatx4 per chunk image
     constexpr int CPT = (C4 + NTHREADS - 1) / NTHREADS;
-    const floatx4* xg4 = (const floatx4*)xg;
+    gfloatx4* xg4 = (gfloatx4*)xg;
     floatx4* xs4w = (floatx4*)Xs;
     for (int k = threadIdx.x; k < C4; k += NTHREADS) xs4w[k] = xg4[k];
     lds_barrier();
@@ -312,42 +317,48 @@ __device__ __forceinline__ void coupling_gemm_xl(const float* __restrict__ xg, c
         b0[t] = ld(t, 0);
         b1[t] = ld(t, 1);
     }
+    // one k-block pair of this chunk (k-blocks kb, kb+1 local; kg0 + .. global)
+    auto kpair = [&](const floatx4* xs4, int kg0, int kb) __attribute__((always_inline)) {
+        floatx4 a = xs4[kb * (XS_BLOCK / 4)];
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+            for (int t = 0; t < TPW; ++t)
+                acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s], b0[t][s], acc[t], 0, 0, 0);
+        const int k2 = kg0 + kb + 2 < NK8 ? kg0 + kb + 2 : NK8 - 1;
+#pragma unroll
+        for (int t = 0; t < TPW; ++t) b0[t] = ld(t, k2);
+        __builtin_amdgcn_sched_barrier(0);
+        a = xs4[(kb + 1) * (XS_BLOCK / 4)];
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+            for (int t = 0; t < TPW; ++t)
+                acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s], b1[t][s], acc[t], 0, 0, 0);
+        const int k3 = kg0 + kb + 3 < NK8 ? kg0 + kb + 3 : NK8 - 1;
+#pragma unroll
+        for (int t = 0; t < TPW; ++t) b1[t] = ld(t, k3);
+        __builtin_amdgcn_sched_barrier(0);
+    };
 #pragma unroll 1
     for (int c = 0; c < nchunk; ++c) {
-        // stage the next chunk in registers while this one multiplies
-        floatx4 nx[CPT];
-        const bool more = c + 1 < nchunk;
-#pragma unroll
-        for (int u = 0; u < CPT; ++u) {
-            const int k = threadIdx.x + u * NTHREADS;
-            if (more && k < C4) nx[u] = xg4[(size_t)(c + 1) * C4 + k];
-        }
         const floatx4* xs4 = reinterpret_cast<const floatx4*>(Xs + (c & 1) * XL_CIMG + (lane >> 5) * XS_HALF +
                                                               (lane & 31) * 4);
         const int kg0 = c * (XL_KC / 8);
-#pragma unroll 1
-        for (int kb = 0; kb < XL_KC / 8; kb += 2) {
-            floatx4 a = xs4[kb * (XS_BLOCK / 4)];
+        const bool more = c + 1 < nchunk;
+        // the next chunk is staged in registers one float4 per k-block pair,
+        // each load issued right after that pair's alpha loads, so the
+        // in-order vmcnt waits of later pairs cover it without a stall
+        floatx4 nx[CPT];
 #pragma unroll
-            for (int s = 0; s < 4; ++s)
-#pragma unroll
-                for (int t = 0; t < TPW; ++t)
-                    acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s], b0[t][s], acc[t], 0, 0, 0);
-            const int k2 = kg0 + kb + 2 < NK8 ? kg0 + kb + 2 : NK8 - 1;
-#pragma unroll
-            for (int t = 0; t < TPW; ++t) b0[t] = ld(t, k2);
-            __builtin_amdgcn_sched_barrier(0);
-            a = xs4[(kb + 1) * (XS_BLOCK / 4)];
-#pragma unroll
-            for (int s = 0; s < 4; ++s)
-#pragma unroll
-                for (int t = 0; t < TPW; ++t)
-                    acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s], b1[t][s], acc[t], 0, 0, 0);
-            const int k3 = kg0 + kb + 3 < NK8 ? kg0 + kb + 3 : NK8 - 1;
-#pragma unroll
-            for (int t = 0; t < TPW; ++t) b1[t] = ld(t, k3);
+        for (int u = 0; u < CPT; ++u) {
+            kpair(xs4, kg0, 2 * u);
+            const int k = threadIdx.x + u * NTHREADS;
+            if (more && k < C4) nx[u] = xg4[(size_t)(c + 1) * C4 + k];
             __builtin_amdgcn_sched_barrier(0);
         }
+#pragma unroll 1
+        for (int kb = 2 * CPT; kb < XL_KC / 8; kb += 2) kpair(xs4, kg0, kb);
         if (more) {  // the other buffer was last read in chunk c-1, before the previous barrier
             floatx4* dst = (floatx4*)(Xs + ((c + 1) & 1) * XL_CIMG);
 #pragma unroll
@@ -625,14 +636,23 @@ struct Part {
 
 typedef __attribute__((address_space(1))) unsigned gu32;
 
-// Arrive at / wait for the group's barrier number ep+1 (Guideline 16 of the
-// CDNA guide: agent-scope release by every storing thread, one agent-scope
-// atomic arrival, a bounded relaxed poll, one agent-scope acquire that drops
-// this CU's stale L1 lines, then the workgroup barrier).  A poll that never
+// Payload stores of a group exchange are write-through (sc1), so the
+// producer needs no L2 write-back (no release fence): CDNA guide,
+// Guideline 16 R1.  The trailing s_nop covers the store-data hazard the
+// compiler cannot see through inline asm.
+__device__ __forceinline__ void store_sc1_x4(float* dst, const floatx4& v) {
+    asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(dst), "v"(v) : "memory");
+}
+
+// Arrive at / wait for the group's barrier number ep+1: every storing wave
+// drains its sc1 payload stores, the workgroup barrier, one agent-scope
+// atomic arrival, a bounded relaxed poll, one agent-scope acquire (drops this
+// CU's L1 lines; L2 is not evicted), the workgroup barrier.  A poll that never
 // completes (a part not resident) gives up after ~1 s and raises stats flag
-// bit 4 instead of hanging the GPU.
+// bit 4 (every later barrier of the launch then gives up at once) instead of
+// hanging the GPU.
 __device__ __noinline__ void group_barrier(const DevParams& p, Part& pt) {
-    __threadfence();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     pt.ep += 1;
     if (threadIdx.x == 0) {
@@ -644,12 +664,15 @@ __device__ __noinline__ void group_barrier(const DevParams& p, Part& pt) {
             __builtin_amdgcn_s_sleep(2);
             // after one timeout every later barrier of the launch gives up at once
             if (++spins > XL_SPIN_MAX ||
-                (__hip_atomic_load(&p.stats[3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 16ull)) {
+                (__hip_atomic_load((__attribute__((address_space(1))) unsigned long long*)&p.stats[3],
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) &
+                 16ull)) {
                 atomicOr(&p.stats[3], 16ull);
                 break;
             }
         }
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __syncthreads();
 }
@@ -661,20 +684,27 @@ template <int NK>
 __device__ __forceinline__ void group_sum(const DevParams& p, Part& pt, float (&vf)[NK], double (&vd)[NK], int nk,
                                           bool with_d) {
     const int tid = threadIdx.x;
-    const size_t base = ((size_t)pt.group * 2 + (pt.ep & 1)) * pt.npart * (RC * E_WG);
+    const int grp = __builtin_amdgcn_readfirstlane(pt.group), npart = __builtin_amdgcn_readfirstlane(pt.npart);
+    const int part = __builtin_amdgcn_readfirstlane(pt.part);
+    const size_t base = ((size_t)grp * 2 + (__builtin_amdgcn_readfirstlane(pt.ep) & 1)) * npart * (RC * E_WG);
     float* xr = p.xred + base;
     double* xd = p.xredd + base;
     if (tid < E_WG)
-        for (int k = 0; k < nk; ++k) {
-            xr[(pt.part * RC + k) * E_WG + tid] = vf[k];
-            if (with_d) xd[(pt.part * RC + k) * E_WG + tid] = vd[k];
+        for (int k = 0; k < nk; ++k) {  // write-through (sc1) stores
+            __hip_atomic_store((gu32*)(xr + (part * RC + k) * E_WG + tid), __float_as_uint(vf[k]),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (with_d)
+                __hip_atomic_store((__attribute__((address_space(1))) unsigned long long*)(xd + (part * RC + k) *
+                                                                                              E_WG + tid),
+                                   (unsigned long long)__double_as_longlong(vd[k]), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
         }
     group_barrier(p, pt);
     if (tid < E_WG)
         for (int k = 0; k < nk; ++k) {
             float a = 0.0f;
             double b = 0.0;
-            for (int q = 0; q < pt.npart; ++q) {
+            for (int q = 0; q < npart; ++q) {
                 a = a + xr[(q * RC + k) * E_WG + tid];
                 if (with_d) b = b + xd[(q * RC + k) * E_WG + tid];
             }
@@ -686,10 +716,11 @@ __device__ __forceinline__ void group_sum(const DevParams& p, Part& pt, float (&
 // Publish this part's sin/cos image (LDS, XL_IMG floats) into the group's
 // image buffer and wait until every part has published its own.
 __device__ __forceinline__ const float* group_publish_x(const DevParams& p, Part& pt, const float* Xs) {
-    const size_t img = ((size_t)pt.group * 2 + (pt.xs_n & 1)) * pt.npart * XL_IMG;
-    floatx4* dst = (floatx4*)(p.xg + img + (size_t)pt.part * XL_IMG);
+    const int grp = __builtin_amdgcn_readfirstlane(pt.group), npart = __builtin_amdgcn_readfirstlane(pt.npart);
+    const size_t img = ((size_t)grp * 2 + (__builtin_amdgcn_readfirstlane(pt.xs_n) & 1)) * npart * XL_IMG;
+    float* dst = uniform_ptr(p.xg + img + (size_t)__builtin_amdgcn_readfirstlane(pt.part) * XL_IMG);
     const floatx4* src = (const floatx4*)Xs;
-    for (int k = threadIdx.x; k < XL_IMG / 4; k += NTHREADS) dst[k] = src[k];
+    for (int k = threadIdx.x; k < XL_IMG / 4; k += NTHREADS) store_sc1_x4(dst + 4 * k, src[k]);
     group_barrier(p, pt);
     pt.xs_n += 1;
     return p.xg + img;
@@ -701,8 +732,8 @@ template <int TPW, bool XL>
 __device__ __forceinline__ void post_step(const DevParams& p, const Slot& ws, int env_base, bool to_ring, Part& pt
                                           STAMP_PARAMS) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, tid = threadIdx.x;
-    const int NG = XL ? pt.ng : TPW * 256;   // oscillators per env
-    const int col0 = XL ? pt.col0 : 0;       // this workgroup's first oscillator
+    const int NG = XL ? __builtin_amdgcn_readfirstlane(pt.ng) : TPW * 256;   // oscillators per env
+    const int col0 = XL ? __builtin_amdgcn_readfirstlane(pt.col0) : 0;       // this workgroup's first oscillator
     float h[8];
 #pragma unroll
     for (int q = 0; q < 8; ++q) h[q] = s_ctl[mfma_env(q, lane)].h;
@@ -974,8 +1005,8 @@ __device__ void solve_wg(const DevParams& p, float* Xs, int env_base, bool to_ri
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, tid = threadIdx.x;
     const int hq = lane >> 5;
     constexpr int N = TPW * 256;            // oscillators owned by this workgroup
-    const int NG = XL ? pt.ng : N;          // oscillators per env
-    const int col0 = XL ? pt.col0 : 0;
+    const int NG = XL ? __builtin_amdgcn_readfirstlane(pt.ng) : N;      // oscillators per env
+    const int col0 = XL ? __builtin_amdgcn_readfirstlane(pt.col0) : 0;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int pair = __builtin_amdgcn_readfirstlane(pt.pair);
     const Slot ws{__builtin_amdgcn_make_buffer_rsrc((void*)uniform_ptr(p.R + (size_t)pair * NSLOT * N * 16), 0,
@@ -1017,8 +1048,8 @@ __device__ void solve_wg(const DevParams& p, float* Xs, int env_base, bool to_ri
         STAMP(1);
         const float* xown = nullptr;
         if constexpr (XL) {
-            const float* xgrp = group_publish_x(p, pt, Xs);   // all parts' images of this stage
-            xown = xgrp + (size_t)pt.part * XL_IMG;
+            const float* xgrp = uniform_ptr(group_publish_x(p, pt, Xs));   // all parts' images of this stage
+            xown = xgrp + (size_t)__builtin_amdgcn_readfirstlane(pt.part) * XL_IMG;
             coupling_gemm_xl<TPW>(xgrp, p.alpha_sw, Xs, NG, col0, acc);
         } else {
             coupling_gemm<TPW>(Xs, p.alpha_sw, acc);
