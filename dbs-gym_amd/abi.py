@@ -55,7 +55,8 @@ class KuraConfig(ctypes.Structure):
         ("n_bins", c_int32),
         ("bins", c_int32 * KURA_MAX_BINS),
         ("padlen", c_int32),
-        ("reserved_i", c_int32 * 4),
+        ("episode_cap", c_int32),
+        ("reserved_i", c_int32 * 3),
         ("dt", c_double),
         ("width", c_double),
         ("pause", c_double),
@@ -92,6 +93,9 @@ _SYMBOLS = {
     "kura_get_state": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "kura_set_state": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "kura_set_env_gain": (c_int, [c_void_p, c_int, c_int, c_void_p]),
+    "kura_psd_bbpow": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int, c_double, c_double, c_double, c_void_p,
+                               c_void_p]),
+    "kura_episode_bbpow": (c_int, [c_void_p, c_void_p, c_double, c_double, c_double, c_void_p, c_void_p]),
     "kura_get_stats": (c_int, [c_void_p, c_void_p, c_int]),
     "kura_get_stamps": (c_int, [c_void_p, c_void_p]),
     "kura_selftest_math": (c_int, [c_void_p, c_void_p, c_void_p, c_int]),

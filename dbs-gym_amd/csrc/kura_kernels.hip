@@ -100,6 +100,10 @@ struct DevParams {
     float* xred;            // [group][2][npart][RC][16] f32 partial sums
     double* xredd;          // [group][2][npart][RC][16] f64 partial sums
     unsigned* gcnt;         // [group][16] arrival counters, zeroed before every launch
+    // episode true-LFP record (cfg.episode_cap > 0): kura_episode_bbpow
+    int episode_cap;
+    float* ep_lfp;          // [B][episode_cap] theta_mean samples of the running episode
+    int* ep_len;            // [B] samples appended since the env's last reset
 };
 
 // Diagnostic phase timers (compile with -DKURA_STAMPS): per wave, cycles
@@ -1376,6 +1380,12 @@ __device__ __forceinline__ void step_pair(const DevParams& p, Part& pt, float* X
             if (lfp_true) lfp_true[(size_t)env * KURA_S_MAX + lane] = lane < S ? s_smp_n[e][lane] : 0.0f;
             if (lfp_rec) lfp_rec[(size_t)env * KURA_S_MAX + lane] = lane < S ? s_smp_r[e][lane] : 0.0;
         }
+        if (p.ep_lfp) {  // episode record: theta_mean of every step (evaluate_HF_DBS.py:83)
+            const int L0 = p.ep_len[env];
+            if (lane < S && L0 + lane < p.episode_cap)
+                p.ep_lfp[(size_t)env * p.episode_cap + L0 + lane] = s_smp_n[e][lane];
+            if (lane == 0) p.ep_len[env] = L0 + S;
+        }
     }
     if (!XL || pt.part == 0) flush_stats(p, rhs, env_base);
 }
@@ -1435,6 +1445,7 @@ __device__ __forceinline__ void reset_pair(const DevParams& p, Part& pt, float* 
             p.t[env] = grid_at_c(s_ctl[e], s_ctl[e].n - 1);
             p.step[env] = 0;
             p.wpos[env] = 0;
+            if (p.ep_len) p.ep_len[env] = 0;  // a new episode starts
         }
         if (obs)
             for (int i = lane; i < W; i += 64) obs[(size_t)env * W + i] = (float)p.ring[(size_t)env * W + i];
@@ -1479,6 +1490,151 @@ __global__ __launch_bounds__(64) void kura_reward_kernel(DevParams p, const doub
     const WinView xv{xl, 0, p.W, 0, 0};
     const double r = reward_of<WPL>(p, x, (double)u0[env], xv, ext, tmp);
     if (lane == 0) out[env] = r;
+}
+
+// ------------------------------------------ episode metric (f) rank 3 ----
+// calc_psd_for_simple_eval (aDBS_RL/evaluate_HF_DBS.py:122-135) of one
+// signal per workgroup: band_pass_envelope's filtfilt (utils.py:794-816, the
+// R2 Butterworth; lane 0, scipy DF2T order), a direct DFT of the bins the
+// beta band and the 12-tap smoothing need (threads own contiguous sample
+// segments; exact start twiddle per segment + complex rotation), |X/n|^2*2,
+// filtfilt(ones(12), 5, .) evaluated on those bins (exact away from the
+// spectrum ends), and the sum over beta_a < f < beta_b.
+#define PSD_THREADS 256
+#define PSD_MAXB 2048
+#define PSD_HALO 12
+
+__device__ void filtfilt_full_dev(const DevParams& p, const float* x, int L, double* ext, double* tmp) {
+    const int P = p.padlen, M = L + 2 * P;
+    const double x0 = (double)x[0], xl = (double)x[L - 1];
+    for (int i = 0; i < P; ++i) ext[i] = 2.0 * x0 - (double)x[P - i];
+    for (int i = 0; i < L; ++i) ext[P + i] = (double)x[i];
+    for (int i = 0; i < P; ++i) ext[P + L + i] = 2.0 * xl - (double)x[L - 2 - i];
+    for (int pass = 0; pass < 2; ++pass) {
+        const double e0 = ext[0];
+        double z0 = p.bw_zi[0] * e0, z1 = p.bw_zi[1] * e0, z2 = p.bw_zi[2] * e0, z3 = p.bw_zi[3] * e0;
+        for (int k = 0; k < M; ++k) {
+            const double xn = ext[k];
+            const double yn = z0 + p.bw_b[0] * xn;
+            z0 = (z1 + xn * p.bw_b[1]) - yn * p.bw_a[1];
+            z1 = (z2 + xn * p.bw_b[2]) - yn * p.bw_a[2];
+            z2 = (z3 + xn * p.bw_b[3]) - yn * p.bw_a[3];
+            z3 = xn * p.bw_b[4] - yn * p.bw_a[4];
+            tmp[k] = yn;
+        }
+        if (pass == 0)
+            for (int i = 0; i < M; ++i) ext[i] = tmp[M - 1 - i];
+    }
+    for (int i = 0; i < L; ++i) ext[i] = tmp[M - 1 - P - i];
+}
+
+__global__ __launch_bounds__(PSD_THREADS) void kura_psd_kernel(DevParams p, const float* __restrict__ sig,
+                                                               const int* __restrict__ lens, long long ld, int j0,
+                                                               int n, int episode, const uint8_t* __restrict__ mask,
+                                                               double psd_dt, double beta_a, double beta_b,
+                                                               double* scratch, long long sld,
+                                                               double* __restrict__ out) {
+    __shared__ double s_ft[PSD_MAXB];
+    __shared__ double s_part[PSD_THREADS / 64][2];
+    const int j = j0 + blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    if (j >= n) return;
+    const double qnan = __builtin_nan("");
+    int L;
+    const float* x;
+    if (episode) {
+        L = p.ep_len[j];
+        x = p.ep_lfp + (size_t)j * p.episode_cap;
+        if ((mask && !mask[j]) || L > p.episode_cap || L < 2) {
+            if (tid == 0) out[j] = qnan;
+            return;
+        }
+    } else {
+        L = lens[j];
+        x = sig + (size_t)j * ld;
+        if (L < 2 || L > ld) {
+            if (tid == 0) out[j] = qnan;
+            return;
+        }
+    }
+    // band bins exactly as np.fft.rfftfreq: f_k = k * (1.0 / (L * psd_dt))
+    const int M = L / 2 + 1;
+    const double val = 1.0 / ((double)L * psd_dt);
+    int k0 = (int)(beta_a / val) - 2, k1 = (int)(beta_b / val) + 2;
+    k0 = k0 < 0 ? 0 : k0;
+    while (k0 < M && !((double)k0 * val > beta_a)) ++k0;
+    k1 = k1 > M - 1 ? M - 1 : k1;
+    while (k1 >= 0 && !((double)k1 * val < beta_b)) --k1;
+    if (k1 < k0) {
+        if (tid == 0) out[j] = 0.0;  // np.sum of an empty selection
+        return;
+    }
+    const int lo = k0 - PSD_HALO, hi = k1 + PSD_HALO, K = hi - lo + 1;
+    // the smoothing filtfilt's odd padding (36 bins) and its 11-bin transients
+    // must stay outside [lo, hi]
+    if (lo < 48 || hi > M - 49 || K > PSD_MAXB) {
+        if (tid == 0) out[j] = qnan;
+        return;
+    }
+    double* ext = scratch + (size_t)blockIdx.x * sld;
+    double* tmp = ext + sld / 2;
+    if (tid == 0) filtfilt_full_dev(p, x, L, ext, tmp);
+    __syncthreads();  // lane 0's global scratch stores are visible workgroup-wide after the barrier
+    const int seg = (L + PSD_THREADS - 1) / PSD_THREADS;
+    const int t0 = tid * seg, t1 = t0 + seg < L ? t0 + seg : L;
+    for (int kk = 0; kk < K; ++kk) {
+        const long long k = lo + kk;
+        double re = 0.0, im = 0.0;
+        if (t0 < t1) {
+            const long long m = (k * (long long)t0) % L;
+            double ws, wc, rs, rc;
+            sincos(-2.0 * M_PI * (double)m / (double)L, &ws, &wc);
+            sincos(-2.0 * M_PI * (double)k / (double)L, &rs, &rc);
+            for (int t = t0; t < t1; ++t) {
+                const double y = ext[t];
+                re = fma(y, wc, re);
+                im = fma(y, ws, im);
+                const double nc = wc * rc - ws * rs;
+                ws = wc * rs + ws * rc;
+                wc = nc;
+            }
+        }
+        re = wave_sum_f64(re);
+        im = wave_sum_f64(im);
+        if (lane == 0) {
+            s_part[wave][0] = re;
+            s_part[wave][1] = im;
+        }
+        __syncthreads();
+        if (tid == 0) {
+            double a = 0.0, b = 0.0;
+            for (int w = 0; w < PSD_THREADS / 64; ++w) {
+                a = a + s_part[w][0];
+                b = b + s_part[w][1];
+            }
+            const double h = hypot(a / (double)L, b / (double)L);
+            s_ft[kk] = h * h * 2.0;
+        }
+        __syncthreads();
+    }
+    if (tid == 0) {
+        // filtfilt(ones(12), 5, ft): b = 1/5 each (lfilter normalises by a[0]),
+        // forward then backward, DF2T association (oldest term innermost)
+        const double bb = 1.0 / 5.0;
+        double* yf = tmp;  // forward output, index kk
+        for (int kk = 11; kk < K; ++kk) {
+            double acc = bb * s_ft[kk - 11];
+            for (int q = 10; q >= 1; --q) acc = acc + bb * s_ft[kk - q];
+            yf[kk] = acc + bb * s_ft[kk];
+        }
+        double tot = 0.0;
+        for (int kk = k0 - lo; kk <= k1 - lo; ++kk) {
+            double acc = bb * yf[kk + 11];
+            for (int q = 10; q >= 1; --q) acc = acc + bb * yf[kk + q];
+            const double zs = acc + bb * yf[kk];
+            tot = tot + zs;
+        }
+        out[j] = tot;
+    }
 }
 
 // ------------------------------------------------------------- self-tests --

@@ -18,7 +18,8 @@ from . import spectral
 from .abi import KURA_S_MAX, KuraConfig, check, ptr
 
 
-def make_config(params: dict, n_envs: int, reward_func: str | None = None, max_steps: int = 4096) -> KuraConfig:
+def make_config(params: dict, n_envs: int, reward_func: str | None = None, max_steps: int = 4096,
+                episode_cap: int = 0) -> KuraConfig:
     """Build the C config from a reference params dict (env.py:277-338)."""
     p = params
     step_len = p["electrode_width"] + p["electrode_pause"]                      # env.py:294
@@ -66,6 +67,7 @@ def make_config(params: dict, n_envs: int, reward_func: str | None = None, max_s
     c.rtol = c.atol = np.float32(1e-5)                                           # env.py:249
     c.kn = np.float32(p["K"] / p["num_oscillators"])                            # env.py:264
     c.dt0 = np.float32(0.05)                                                     # env.py:267
+    c.episode_cap = int(episode_cap)
     return c
 
 
@@ -155,6 +157,35 @@ class KuraSim:
         with torch.cuda.device(self.device):
             check(self.lib, self.lib.kura_reward(self._h, int(kind), ptr(w), ptr(u), ptr(out), n, self._stream()),
                   "kura_reward")
+        return out
+
+    # ---- episode evaluation metric (aDBS_RL/evaluate_HF_DBS.py:122-135) ---------
+    def psd_bbpow(self, signals, psd_dt: float = 5e-4, beta=(12.5, 21.0)) -> np.ndarray:
+        """calc_psd_for_simple_eval of arbitrary float32 signals (list of 1-D arrays)."""
+        n = len(signals)
+        ld = max(2, max(len(x) for x in signals))
+        buf = np.zeros((n, ld), np.float32)
+        for j, x in enumerate(signals):
+            buf[j, :len(x)] = x
+        lens = torch.tensor([len(x) for x in signals], dtype=torch.int32, device=self.device)
+        sig = torch.from_numpy(buf).to(self.device)
+        out = torch.empty(n, dtype=torch.float64, device=self.device)
+        with torch.cuda.device(self.device):
+            check(self.lib, self.lib.kura_psd_bbpow(self._h, ptr(sig), ptr(lens), ld, n, float(psd_dt),
+                                                    float(beta[0]), float(beta[1]), ptr(out), self._stream()),
+                  "kura_psd_bbpow")
+        return out.cpu().numpy()
+
+    def episode_bbpow(self, mask: torch.Tensor | None = None, psd_dt: float = 5e-4,
+                      beta=(12.5, 21.0)) -> torch.Tensor:
+        """The same metric of each env's running episode (config.episode_cap > 0)."""
+        out = torch.empty(self.B, dtype=torch.float64, device=self.device)
+        m = None if mask is None else mask.to(self.device, torch.uint8).contiguous()
+        with torch.cuda.device(self.device):
+            check(self.lib, self.lib.kura_episode_bbpow(self._h, ptr(m), float(psd_dt), float(beta[0]),
+                                                        float(beta[1]), ptr(out), self._stream()),
+                  "kura_episode_bbpow")
+        self._keep_mask = m
         return out
 
     # ---- state ------------------------------------------------------------------

@@ -57,7 +57,8 @@ class KuraVectorEnv:
     metadata = {"render.modes": ["human"]}
 
     def __init__(self, params, num_envs: int | None = None, device=0, reward_func: str | None = None,
-                 w0_seed: int = 228, rand_seeds=None, autoreset: bool = True, max_steps: int = 4096):
+                 w0_seed: int = 228, rand_seeds=None, autoreset: bool = True, max_steps: int = 4096,
+                 episode_metrics: bool = False, psd_dt: float = 5e-4, beta_band=(12.5, 21.0)):
         if isinstance(params, dict):
             if num_envs is None:
                 raise ValueError("num_envs is required with a single params dict")
@@ -78,7 +79,11 @@ class KuraVectorEnv:
         self.params = plist
         self.num_envs = B = num_envs
         self.hosts, shared = build_batch(plist)
-        self.cfg = make_config(plist[0], B, reward_func=plist[0]["reward_func"], max_steps=max_steps)
+        ep_steps = int(plist[0]["total_episode_len"] / (plist[0]["electrode_width"] + plist[0]["electrode_pause"]))
+        self.cfg = make_config(plist[0], B, reward_func=plist[0]["reward_func"], max_steps=max_steps,
+                               episode_cap=(ep_steps + 1) * KURA_S_MAX if episode_metrics else 0)
+        self.episode_metrics = episode_metrics
+        self.psd_dt, self.beta_band = psd_dt, tuple(beta_band)
         self.sim = KuraSim(self.cfg, device)
         self.device = self.sim.device
         self.sim.set_coupling(shared["alpha"].astype(np.float32))
@@ -137,11 +142,17 @@ class KuraVectorEnv:
         infos: dict = {}
         term_host = self.steps >= self.episode_steps
         terminated = done.bool().clone()
-        if self.autoreset and term_host.any():
+        if term_host.any():
             idx = np.nonzero(term_host)[0]
-            infos["terminal_observation"] = obs[torch.as_tensor(idx, device=self.device)].clone().view(-1, 1, self.W)
             infos["terminal_env_ids"] = idx
             infos["episode"] = {"l": self.steps[idx].copy()}
+            if self.episode_metrics:  # calc_psd_for_simple_eval of the finished episodes (evaluate_HF_DBS.py:106)
+                mask = torch.zeros(self.num_envs, dtype=torch.uint8)
+                mask[idx] = 1
+                bb = self.sim.episode_bbpow(mask, self.psd_dt, self.beta_band)
+                infos["episode"]["bbpow"] = bb[torch.as_tensor(idx, device=self.device)].cpu().numpy()
+        if self.autoreset and term_host.any():
+            infos["terminal_observation"] = obs[torch.as_tensor(idx, device=self.device)].clone().view(-1, 1, self.W)
             mask = torch.zeros(self.num_envs, dtype=torch.uint8)
             mask[idx] = 1
             th = self._draw(idx)

@@ -64,7 +64,9 @@ typedef struct KuraConfig {
     int32_t n_bins;        /* rfft bins with beta_a < f < beta_b (utils.py:24-26) */
     int32_t bins[KURA_MAX_BINS];
     int32_t padlen;        /* filtfilt padlen for R2 (3*max(len(a),len(b)) = 15) */
-    int32_t reserved_i[4];
+    int32_t episode_cap;   /* >0: keep each env's true-LFP samples of the running episode (up to this
+                              many) for kura_episode_bbpow (evaluate_HF_DBS.py:83,122-135); 0: off */
+    int32_t reserved_i[3];
     double dt;             /* verbose_dt: save-grid spacing (units) */
     double width;          /* electrode_width: stimulation ON interval */
     double pause;          /* electrode_pause: OFF interval */
@@ -95,6 +97,22 @@ int kura_set_env_params(KuraHandle* h, int env0, int n,
                         const float* omega,   /* n*N  (float32 cast of w0, env.py:264) */
                         const double* g_stim, /* n*n_elec*N conductances, env.py:106-120 */
                         const double* g_rec); /* n*n_rec*N  recorder conductances, :142-156 */
+/* calc_psd_for_simple_eval (aDBS_RL/evaluate_HF_DBS.py:122-135) of n device
+ * signals sig[j*ld ...] of len[j] float32 samples (an episode's concatenated
+ * true LFP): band_pass_envelope filtfilt (butter(2, [12,30]/(fs/2))), |rfft/n|^2*2,
+ * filtfilt(ones(12), 5, .) smoothing, sum over beta_a < f < beta_b with
+ * f = k/(len*psd_dt).  out[j] (device f64) is NaN when the band lies within
+ * 48 bins of either spectrum end (too short a signal).  Float64 throughout;
+ * agrees with NumPy/SciPy to ~1e-12 relative (not bitwise: FFT vs direct DFT). */
+int kura_psd_bbpow(KuraHandle* h, const float* sig, const int32_t* len, int64_t ld, int n, double psd_dt,
+                   double beta_a, double beta_b, double* out, void* stream);
+/* the same metric of every env's current-episode true LFP (requires
+ * cfg.episode_cap > 0); mask[b] (device, NULL = all) selects envs; out[b]
+ * NaN for unselected envs and for episodes longer than episode_cap.  Call it
+ * after the last kura_step of an episode and before the kura_reset that
+ * starts the next one (KuraVectorEnv does so for autoreset envs). */
+int kura_episode_bbpow(KuraHandle* h, const uint8_t* mask, double psd_dt, double beta_a, double beta_b,
+                       double* out, void* stream);
 /* per-env coupling gain float32(K_b / N) for envs [env0, env0+n) (host
  * array; each reference env has its own params_dict['K'], env.py:264).  Envs
  * not set keep the config's kn. */

@@ -1,0 +1,75 @@
+"""Episode evaluation metric: calc_psd_for_simple_eval.
+
+CPU: the restatement oracle/kura_eval.py against the reference function's own
+outputs (tests/golden/make_golden_eval.py).  GPU: kura_psd_bbpow and the
+per-env episode record (KuraVectorEnv(episode_metrics=True)) against the
+restatement; float64 with a direct DFT instead of pocketfft, so the bar is
+relative 1e-10, not bitwise."""
+import hashlib
+import importlib
+import os
+import sys
+
+import numpy as np
+import pytest
+
+from helpers import ROOT, kura
+
+sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+from make_golden_eval import signals  # noqa: E402
+from oracle import kura_eval  # noqa: E402
+
+G = np.load(os.path.join(ROOT, "tests", "golden", "reference_eval_golden.npz"))
+RTOL = 1e-10
+
+
+def test_signals_regenerate_exactly():
+    for s, n, h in zip(signals(), G["psd_len"], G["psd_sig_sha1"]):
+        assert len(s) == n and hashlib.sha1(s.tobytes()).hexdigest() == str(h)
+
+
+def test_restatement_matches_reference():
+    got = kura_eval.calc_psd_for_simple_eval(signals(), float(G["psd_dt"]))
+    np.testing.assert_allclose(got, G["psd_bbpow"], rtol=1e-12, atol=0)
+
+
+@pytest.mark.gpu
+def test_gpu_psd_bbpow_matches_reference():
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    sim_mod = importlib.import_module("dbs-gym_amd.sim")
+    cfg = sim_mod.make_config(kura.reference_params("env0"), 4, reward_func="bbpow_action")
+    sim = sim_mod.KuraSim(cfg, 0)
+    sig = signals()
+    got = sim.psd_bbpow(sig, psd_dt=float(G["psd_dt"]))
+    np.testing.assert_allclose(got, G["psd_bbpow"], rtol=RTOL, atol=0)
+    # too short for the band to clear the spectrum ends -> NaN, not a wrong value
+    assert np.isnan(sim.psd_bbpow([sig[0][:2000]])[0])
+    sim.close()
+
+
+@pytest.mark.gpu
+def test_gpu_episode_record_metric():
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    vec = importlib.import_module("dbs-gym_amd.vec_env")
+    p = kura.synthetic_params("env0", 256)
+    B, steps = 3, 560
+    env = vec.KuraVectorEnv(p, num_envs=B, episode_metrics=True, w0_seed=5, reward_func="bbpow_action")
+    env.episode_steps = steps
+    env.reset(seed=3)
+    rng = np.random.default_rng(1)
+    lfp = [[] for _ in range(B)]
+    info = {}
+    for k in range(steps):
+        a = rng.uniform(-1, 1, (B, 1)).astype(np.float32)
+        obs, rew, term, trunc, info = env.step(a)
+        tm = env.get_attr("theta_mean")
+        for b in range(B):
+            lfp[b].append(tm[b])
+    ref = kura_eval.calc_psd_for_simple_eval([np.concatenate(x) for x in lfp], 5e-4)
+    got = info["episode"]["bbpow"]
+    np.testing.assert_allclose(got, ref, rtol=RTOL, atol=0)
+    env.close()
