@@ -104,11 +104,7 @@ class EnvHost:
         g_stim = ms.conductances(self.grid, gs, self.elec_coords, self.encapsulation_coeff, naive)
         g_rec = ms.conductances(self.grid, gs, self.rec_coords, self.encapsulation_coeff, naive)
         if p.get("directed_stimulation"):                                      # env.py:125-140
-            masks = []
-            for c in self.elec_coords:
-                idx = ms.flat_index(c, gs)
-                masks.append(ms.directed_stim_masks(self.grid, np.asarray(c), idx)[0])
-            g_stim = g_stim * np.stack(masks)
+            g_stim = ms.directed_conductances(self.grid, gs, self.elec_coords, g_stim)
         theta0 = ms.initial_phases(self.rs, self.N, p["init_state_mean"], p["init_state_sd"])  # env.py:595-598
         return w0, g_stim, g_rec, theta0
 

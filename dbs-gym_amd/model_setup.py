@@ -190,3 +190,13 @@ def directed_stim_masks(grid_points, center, center_idx):
     for m in (m1, m2, m3):
         m[center_idx] = True
     return m1, m2, m3
+
+
+def directed_conductances(neur_grid, grid_size, elec_coords, g_stim) -> np.ndarray:
+    """SimpleDBS directional stimulation (env.py:125-140): every contact's
+    conductance times the first 120-degree sector around that contact.  As in
+    the reference, the sector's forced-on centre is the LAST contact's index
+    (the loop variable elec_idx left over from env.py:93-95) for every contact."""
+    last_idx = flat_index(elec_coords[-1], grid_size)
+    masks = [directed_stim_masks(neur_grid, np.asarray(c), last_idx)[0] for c in elec_coords]
+    return np.asarray(g_stim) * np.stack(masks)

@@ -15,14 +15,14 @@ kura = importlib.import_module("dbs-gym_amd")
 from oracle import kura_oracle as ko  # noqa: E402
 
 
-def make_case(name="env0", n_osc=512, n_envs=4, reward="bbpow_action", seed=0, split="train"):
+def make_case(name="env0", n_osc=512, n_envs=4, reward="bbpow_action", seed=0, split="train", **overrides):
     """Returns (cfg, alpha_f32, omega, g_stim, g_rec, theta0, ctab, stab, hosts)."""
     from importlib import import_module
     sim = import_module("dbs-gym_amd.sim")
     if n_osc == 512:
-        base = kura.reference_params(name, split)
+        base = kura.reference_params(name, split, **overrides)
     else:
-        base = kura.synthetic_params(name, n_osc)
+        base = kura.synthetic_params(name, n_osc, **overrides)
     plist = []
     for b in range(n_envs):
         p = dict(base)

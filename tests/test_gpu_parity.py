@@ -66,9 +66,9 @@ def test_mfma_gemm_is_fmaf_chain(lib, N):
     np.testing.assert_array_equal(Y, ko.gemm_chain(X, A))
 
 
-def _run_pair(torch, name, N, B, reward, steps, act, check_every=1, gains=None):
+def _run_pair(torch, name, N, B, reward, steps, act, check_every=1, gains=None, **overrides):
     sim_mod = importlib.import_module("dbs-gym_amd.sim")
-    cfg, alpha, omega, gs, gr, th0, ct, st, _ = make_case(name, N, B, reward=reward)
+    cfg, alpha, omega, gs, gr, th0, ct, st, _ = make_case(name, N, B, reward=reward, **overrides)
     sim = sim_mod.KuraSim(cfg, 0)
     sim.set_coupling(alpha)
     sim.set_env_params(omega, gs, gr)
@@ -126,6 +126,13 @@ def test_step_parity_random_gain(torch_gpu):
     N, B = 512, 19
     gains = (rng.uniform(0.3, 0.8, B) / N).astype(np.float32)
     g, o = _run_pair(torch_gpu, "env0", N, B, "bbpow_action", 8, "rand", gains=gains)
+    np.testing.assert_array_equal(g["y"], o["y"])
+
+
+def test_step_parity_wavelet_directed(torch_gpu):
+    """SURVEY 8(f) rank 4 options: wavelet coupling (signed alpha) + directional stimulation."""
+    g, o = _run_pair(torch_gpu, "env0", 512, 19, "bbpow_action", 6, "hf", spatial_kernel="wavelet",
+                     wavelet_amp=2.0, wavelet_steepness=0.5, directed_stimulation=True)
     np.testing.assert_array_equal(g["y"], o["y"])
 
 
