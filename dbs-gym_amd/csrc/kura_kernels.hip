@@ -104,6 +104,7 @@ struct DevParams {
     int episode_cap;
     float* ep_lfp;          // [B][episode_cap] theta_mean samples of the running episode
     int* ep_len;            // [B] samples appended since the env's last reset
+    int desync_cycles;      // odd workgroups start this many cycles late (spreads record bursts)
 };
 
 // Diagnostic phase timers (compile with -DKURA_STAMPS): per wave, cycles
@@ -479,7 +480,7 @@ __device__ __forceinline__ void store8(const Slot& w, int slot, int t, const flo
 template <int TPW, bool XL>
 __device__ __forceinline__ void coupling_epilogue(const DevParams& p, const Slot& ws, const float* __restrict__ Xs,
                                                   const float* __restrict__ xown, const floatx16 (&acc)[TPW],
-                                                  int stage, bool pulse_on) {
+                                                  int stage, bool pulse_on, float (&fout)[TPW][8]) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     float w[TPW][8], u[TPW][8];
 #pragma unroll
@@ -514,6 +515,7 @@ __device__ __forceinline__ void coupling_epilogue(const DevParams& p, const Slot
             const float tq = sn * Q;
             const float coup = __builtin_fmaf(cs, P, -tq);
             f[q] = __builtin_fmaf(knq[q], coup, w[t][q]) + u[t][q];
+            fout[t][q] = f[q];
         }
         store8(ws, SL_F0 + stage, t, f);
     }
@@ -521,70 +523,69 @@ __device__ __forceinline__ void coupling_epilogue(const DevParams& p, const Slot
 
 // Stage input ys = y0 + chain_j(A[s][j] * h*f_j) (zero coefficients skipped,
 // as in the oracle), theta = fmod(ys, 2pi), sin/cos into the LDS operand.
-// Stage 0 is the solve's initial RHS at y0.  Column tiles are processed two at
-// a time so the records of both are in flight before any use.
-template <int NT>
-__device__ __forceinline__ void stage_tiles(const Slot& ws, float* Xs, int s, const float (&h)[8], int t0) {
+// Stage 0 is the solve's initial RHS at y0.  Tiles are software-pipelined:
+// the records of tile t+1 are requested before tile t is computed, and the
+// newest f (f_{s-1}, still in registers from the epilogue) is not reloaded
+// when have_prev.
+template <int TPW>
+__device__ __forceinline__ void stage_input(const Slot& ws, float* Xs, int s, const float (&fprev)[TPW][8],
+                                            bool have_prev STAMP_PARAMS) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int TPW = ws.N / 256;
-    float y0[NT][8], f[NT][6][8];
+    float h[8];
 #pragma unroll
-    for (int u = 0; u < NT; ++u) {
-        load8(ws, SL_Y0, t0 + u, y0[u]);
+    for (int q = 0; q < 8; ++q) h[q] = s_ctl[mfma_env(q, lane)].h;
+    const int nmem = have_prev ? s - 1 : s;  // f_0 .. f_{nmem-1} come from the records
+    float y0[2][8], f[2][6][8];
+    auto fetch = [&](int t, int b) __attribute__((always_inline)) {
+        load8(ws, SL_Y0, t, y0[b]);
 #pragma unroll
         for (int j = 0; j < 6; ++j)
-            if (j < s) load8(ws, SL_F0 + j, t0 + u, f[u][j]);
-    }
-    float ys[NT][8], th[NT][8];
-    int slow = 0;
+            if (j < nmem) load8(ws, SL_F0 + j, t, f[b][j]);
+    };
+    fetch(0, 0);
 #pragma unroll
-    for (int u = 0; u < NT; ++u) {
+    for (int t = 0; t < TPW; ++t) {
+        const int b = t & 1;
+        if (t + 1 < TPW) fetch(t + 1, b ^ 1);
+        if (have_prev) {
+#pragma unroll
+            for (int q = 0; q < 8; ++q) f[b][5][q] = fprev[t][q];  // f_{s-1}; slot 5 is unused when have_prev
+        }
+        const int i = 32 * (wave * TPW + t) + (lane & 31);
+        float ys[8], th[8];
+        int slow = 0;
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
-            float v = y0[u][q];
+            float v = y0[b][q];
             if (s > 0) {
-                float acc = cA[s][0] * (h[q] * f[u][0][q]);
-                if (s > 1 && cA[s][1] != 0.0f) acc = __builtin_fmaf(cA[s][1], h[q] * f[u][1][q], acc);
-                if (s > 2) acc = __builtin_fmaf(cA[s][2], h[q] * f[u][2][q], acc);
-                if (s > 3) acc = __builtin_fmaf(cA[s][3], h[q] * f[u][3][q], acc);
-                if (s > 4) acc = __builtin_fmaf(cA[s][4], h[q] * f[u][4][q], acc);
-                if (s > 5) acc = __builtin_fmaf(cA[s][5], h[q] * f[u][5][q], acc);
-                v = y0[u][q] + acc;
+                // term j: f_j from the records, or (j == s-1, have_prev) from the epilogue
+#define KURA_FJ(j) ((have_prev && (j) == s - 1) ? f[b][5][q] : f[b][j][q])
+                float acc = cA[s][0] * (h[q] * KURA_FJ(0));
+                if (s > 1 && cA[s][1] != 0.0f) acc = __builtin_fmaf(cA[s][1], h[q] * KURA_FJ(1), acc);
+                if (s > 2) acc = __builtin_fmaf(cA[s][2], h[q] * KURA_FJ(2), acc);
+                if (s > 3) acc = __builtin_fmaf(cA[s][3], h[q] * KURA_FJ(3), acc);
+                if (s > 4) acc = __builtin_fmaf(cA[s][4], h[q] * KURA_FJ(4), acc);
+                if (s > 5) acc = __builtin_fmaf(cA[s][5], h[q] * KURA_FJ(5), acc);
+#undef KURA_FJ
+                v = y0[b][q] + acc;
             }
-            ys[u][q] = v;
-            th[u][q] = kdm_fmod2pi_fast(v, &slow);
+            ys[q] = v;
+            th[q] = kdm_fmod2pi_fast(v, &slow);
         }
-    }
-    if (__builtin_expect(__any(slow), 0)) {  // |y| >= 2^22: never in practice
+        if (__builtin_expect(__any(slow), 0)) {  // |y| >= 2^22: never in practice
 #pragma unroll
-        for (int u = 0; u < NT; ++u)
-#pragma unroll
-            for (int q = 0; q < 8; ++q) th[u][q] = kdm_fmod2pi(ys[u][q]);
-    }
-#pragma unroll
-    for (int u = 0; u < NT; ++u) {
-        const int i = 32 * (wave * TPW + t0 + u) + (lane & 31);
+            for (int q = 0; q < 8; ++q) th[q] = kdm_fmod2pi(ys[q]);
+        }
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
             float sn, cs;
-            kdm_sincosf(th[u][q], &sn, &cs);
+            kdm_sincosf(th[q], &sn, &cs);
             const int e = mfma_env(q, lane);
             Xs[xs_idx(e, i)] = sn;
             Xs[xs_idx(16 + e, i)] = cs;
         }
-        if (s == 6) store8(ws, SL_Y1, t0 + u, ys[u]);
+        if (s == 6) store8(ws, SL_Y1, t, ys);
     }
-}
-
-template <int TPW>
-__device__ __forceinline__ void stage_input(const Slot& ws, float* Xs, int s) {
-    const int lane = threadIdx.x & 63;
-    float h[8];
-#pragma unroll
-    for (int q = 0; q < 8; ++q) h[q] = s_ctl[mfma_env(q, lane)].h;
-    constexpr int NT = TPW < 2 ? TPW : 2;
-#pragma unroll 1
-    for (int t = 0; t < TPW; t += NT) stage_tiles<NT>(ws, Xs, s, h, t);
 }
 
 // RM reduction (kura_detmath.h): per-lane partials (t order) -> 32-lane xor
@@ -1044,10 +1045,11 @@ __device__ void solve_wg(const DevParams& p, float* Xs, int env_base, bool to_ri
     STAMP_DECL
     long long nrhs = 0;
     int s = 0;  // stage 0 = initial RHS at y0 (FSAL seed)
+    float fcur[TPW][8];
+    stage_input<TPW>(ws, Xs, 0, fcur, false STAMP_ARGS);
+    STAMP(0);
     for (;;) {
         floatx16 acc[TPW];
-        stage_input<TPW>(ws, Xs, s);
-        STAMP(0);
         lds_barrier();
         STAMP(1);
         const float* xown = nullptr;
@@ -1059,13 +1061,15 @@ __device__ void solve_wg(const DevParams& p, float* Xs, int env_base, bool to_ri
             coupling_gemm<TPW>(Xs, p.alpha_sw, acc);
         }
         STAMP(2);
-        coupling_epilogue<TPW, XL>(p, ws, Xs, xown, acc, s, pulse_on);
+        coupling_epilogue<TPW, XL>(p, ws, Xs, xown, acc, s, pulse_on, fcur);
         STAMP(3);
-        lds_barrier();
+        lds_barrier();  // every wave is done reading the operand before it is rewritten
         STAMP(4);
         ++nrhs;
         if (s > 0 && s < 6) {
             ++s;
+            stage_input<TPW>(ws, Xs, s, fcur, true STAMP_ARGS);   // f_{s-1} straight from the epilogue
+            STAMP(0);
             continue;
         }
         if (s == 6) {
@@ -1082,7 +1086,12 @@ __device__ void solve_wg(const DevParams& p, float* Xs, int env_base, bool to_ri
         lds_barrier();
         STAMP(6);
         if (s_any == 0) break;
+        // stage 1 of the next Dopri step: after stage 0 f_0 is still in
+        // registers; after a step f_0 is the FSAL select of post_step (records)
+        const bool prev = s == 0;
         s = 1;
+        stage_input<TPW>(ws, Xs, 1, fcur, prev STAMP_ARGS);
+        STAMP(0);
     }
     STAMP_FLUSH(p);
     *rhs_count += nrhs;
@@ -1261,6 +1270,12 @@ __device__ __forceinline__ void step_pair(const DevParams& p, Part& pt, float* X
     const int env_base = pt.group * E_WG;
     const int c0 = XL ? pt.col0 : 0, c1 = XL ? pt.col0 + XL_NL : N;   // oscillators of this workgroup
     __syncthreads();  // previous pair's LDS readers
+    if (!XL && p.desync_cycles > 0 && (blockIdx.x & 1)) {
+        // every workgroup runs the same phase sequence, so without an offset
+        // all CUs hit the record traffic of a stage input at the same time
+        const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+        while (__builtin_amdgcn_s_memtime() - t0 < (unsigned long long)p.desync_cycles) __builtin_amdgcn_s_sleep(8);
+    }
     ctl_clear();
     // ---- thread e: rescale_action (env.py:389-393), ON grid (env.py:426-428)
     if (tid < E_WG) {

@@ -15,7 +15,7 @@ import __graft_entry__ as ge  # noqa: E402
 
 LIB = os.path.join(ge.CSRC, "libkura_stamps.so")
 PHASES = ["stage_input", "barrier1", "gemm", "epilogue", "barrier2", "post_err", "flag_sync", "post_decide",
-          "post_saves", "post_fsal", "post_time", "s11", "s12", "s13", "s14", "s15"]
+          "post_saves", "post_fsal", "post_time", "si_wait", "s12", "s13", "s14", "s15"]
 
 
 def main():
