@@ -431,8 +431,11 @@ __device__ __forceinline__ void ctl_begin(CtlE& c, const Grid& g, float dt0, int
 // MFMA-layout element ownership: lane holds, for each of its TPW column tiles
 // t, accumulator rows q = 0..7 (sin rows) and q+8 (cos rows) of local env
 // e(q) = (q&3) + 8(q>>2) + 4(lane>>5) at column i = 32(wave*TPW + t) + (lane&31).
-// Workspace records are [slot][i][16 envs] per workgroup, so q = 0..3 and
-// q = 4..7 are two 16-byte vectors at envs 4h.. and 8+4h...
+// Workspace records are [slot][column tile][half][lane][4] per workgroup: a
+// 2 KiB tile holds the 32 columns x 16 envs a wave's tile touches, laid out so
+// that each of the two 16-byte vectors a lane loads (q = 0..3: envs 4h..4h+3,
+// q = 4..7: envs 8+4h..) sits at lane*16 in its 1 KiB half -- every record
+// load/store instruction covers 8 whole 128-byte lines.
 __device__ __forceinline__ int mfma_env(int q, int lane) { return (q & 3) + 8 * (q >> 2) + 4 * (lane >> 5); }
 
 enum { SL_Y0 = 0, SL_F0 = 1, SL_Y1 = 8, SL_CA = 9, SL_CB = 10, SL_CC = 11, SL_W = 12, SL_P = 13, NSLOT = 14 };
@@ -446,7 +449,7 @@ struct Slot {
     __amdgpu_buffer_rsrc_t rs;
     int N;
     int ct0;   // first column tile of this wave (wave * TPW), wave-uniform
-    int voff;  // (lane & 31) * 64 + (lane >> 5) * 16 bytes
+    int voff;  // lane * 16 bytes (half 0); half 1 at +1024
     gfloat* base;
     __device__ int soff(int slot, int t) const { return (slot * N + 32 * (ct0 + t)) * 64; }
 };
@@ -459,7 +462,7 @@ __device__ __forceinline__ void split8(const floatx4& a, const floatx4& b, float
 __device__ __forceinline__ void load8(const Slot& w, int slot, int t, float (&v)[8]) {
     const floatx4 a = __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(w.rs, w.voff, w.soff(slot, t), 0));
     const floatx4 b =
-        __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(w.rs, w.voff + 32, w.soff(slot, t), 0));
+        __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(w.rs, w.voff + 1024, w.soff(slot, t), 0));
     split8(a, b, v);
 }
 __device__ __forceinline__ void store8(const Slot& w, int slot, int t, const float (&v)[8]) {
@@ -470,7 +473,7 @@ __device__ __forceinline__ void store8(const Slot& w, int slot, int t, const flo
     const floatx4 a = {v[0], v[1], v[2], v[3]}, b = {v[4], v[5], v[6], v[7]};
     __attribute__((address_space(1))) char* sb = (__attribute__((address_space(1))) char*)w.base + w.soff(slot, t);
     *(gfx4*)(sb + (uint32_t)w.voff) = a;
-    *(gfx4*)(sb + (uint32_t)(w.voff + 32)) = b;
+    *(gfx4*)(sb + (uint32_t)(w.voff + 1024)) = b;
 }
 
 // f = fmaf(kn, fmaf(c, P, -(s*Q)), omega) + pulse  ->  slot F0 + stage
@@ -1008,7 +1011,6 @@ template <int TPW, bool XL>
 __device__ void solve_wg(const DevParams& p, float* Xs, int env_base, bool to_ring, bool pulse_on,
                          long long* rhs_count, Part& pt) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, tid = threadIdx.x;
-    const int hq = lane >> 5;
     constexpr int N = TPW * 256;            // oscillators owned by this workgroup
     const int NG = XL ? __builtin_amdgcn_readfirstlane(pt.ng) : N;      // oscillators per env
     const int col0 = XL ? __builtin_amdgcn_readfirstlane(pt.col0) : 0;
@@ -1016,7 +1018,7 @@ __device__ void solve_wg(const DevParams& p, float* Xs, int env_base, bool to_ri
     const int pair = __builtin_amdgcn_readfirstlane(pt.pair);
     const Slot ws{__builtin_amdgcn_make_buffer_rsrc((void*)uniform_ptr(p.R + (size_t)pair * NSLOT * N * 16), 0,
                                                     NSLOT * N * 16 * 4, 0x00020000),
-                  N, wv * TPW, (lane & 31) * 64 + hq * 16,
+                  N, wv * TPW, lane * 16,
                   (gfloat*)uniform_ptr(p.R + (size_t)pair * NSLOT * N * 16)};
     // records y0 <- state y, omega, pulse (0 while stimulation is OFF, env.py:434)
 #pragma unroll 1
