@@ -15,7 +15,7 @@ import __graft_entry__ as ge  # noqa: E402
 
 LIB = os.path.join(ge.CSRC, "libkura_stamps.so")
 PHASES = ["stage_input", "barrier1", "gemm", "epilogue", "barrier2", "post_err", "flag_sync", "post_decide",
-          "post_saves", "post_fsal", "post_time", "si_wait", "s12", "s13", "s14", "s15"]
+          "post_saves", "post_fsal", "post_time", "gemm_p2", "hooks", "s13", "s14", "s15"]
 
 
 def main():
@@ -58,7 +58,10 @@ def main():
     cyc_per_step_wave = s.sum(axis=0) / (8 * nwg * nsteps)
     out = {"ms_per_step": ev0.elapsed_time(ev1) / nsteps,
            "share": dict(zip(PHASES, [round(float(x), 4) for x in share])),
-           "cycles_per_step_per_wave": dict(zip(PHASES, [round(float(x)) for x in cyc_per_step_wave]))}
+           "cycles_per_step_per_wave": dict(zip(PHASES, [round(float(x)) for x in cyc_per_step_wave])),
+           # per wave (rows), cycles per step of the phases that differ between waves
+           "per_wave": {PHASES[k]: [round(float(v)) for v in s[:, k] / (nwg * nsteps)]
+                        for k in range(len(PHASES)) if s[:, k].sum() > 0}}
     print(json.dumps(out))
 
 
