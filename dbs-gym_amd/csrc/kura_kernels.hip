@@ -392,11 +392,12 @@ struct CtlE {
 };
 __shared__ CtlE s_ctl[E_WG];
 __shared__ float s_kn[E_WG];  // per-env coupling gain of the workgroup's envs
-#define RC 4  // save rounds evaluated per pass over the records
-__shared__ float s_red[RC][NWAVES][E_WG];        // per-wave partial sums (f32)
+#define RC 4     // save rounds per pass over the records: recorder (f64) LFP, split groups
+#define RC_N 8   // ... naive LFP on one workgroup per env group (f32 partials only)
+__shared__ float s_red[RC_N][NWAVES][E_WG];      // per-wave partial sums (f32)
 __shared__ double s_redd[RC][NWAVES][E_WG];      // per-wave partial sums (f64, recorder LFP)
-__shared__ float s_theta[E_WG][RC];              // dense-output abscissae of the rounds of a pass
-__shared__ int s_rflag[E_WG][RC];                // bit0: save row, bit1: LFP row, bit2: final row
+__shared__ float s_theta[E_WG][RC_N];            // dense-output abscissae of the rounds of a pass
+__shared__ int s_rflag[E_WG][RC_N];              // bit0: save row, bit1: LFP row, bit2: final row
 __shared__ double s_u[E_WG][4];                  // rescaled amplitudes (env.py:389-393)
 __shared__ int s_maxsave, s_any;
 
@@ -736,12 +737,155 @@ __device__ __forceinline__ const float* group_publish_x(const DevParams& p, Part
 
 // After the 7th stage: error norm, accept/reject, dense-output saves with
 // LFP, FSAL -- for all 16 envs, every wave on its own columns.
+// One pass of post_step's saves: rounds r0 .. r0+nk-1 (nk = min(RCX, nrounds - r0))
+// evaluated from the dense-output records of every tile, LFP partials reduced
+// in RM order, samples stored by thread e.  RCX is a compile-time bound on the
+// rounds of a pass (register arrays); rounds past nk are skipped.
+template <int TPW, bool XL, int RCX>
+__device__ __forceinline__ void save_pass(const DevParams& p, const Slot& ws, int env_base, bool to_ring, Part& pt,
+                                          const float (&h)[8], int r0, int nrounds, bool gauss) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, tid = threadIdx.x;
+    const int NG = XL ? __builtin_amdgcn_readfirstlane(pt.ng) : TPW * 256;
+    const int col0 = XL ? __builtin_amdgcn_readfirstlane(pt.col0) : 0;
+    const int nk = nrounds - r0 < RCX ? nrounds - r0 : RCX;
+    // per-round flag bits, 3 per round: LFP rows, and LFP or final rows
+    constexpr int kLfp = (int)(02222222222u & ((1u << (3 * RCX)) - 1u));
+    constexpr int kEval = (int)(06666666666u & ((1u << (3 * RCX)) - 1u));
+    if (tid < E_WG) {
+        const CtlE& c = s_ctl[tid];
+        for (int k = 0; k < RCX; ++k) {
+            const int r = r0 + k;
+            int fl = 0;
+            float th = 0.0f;
+            if (r < c.nsave) {
+                const int si = c.si + r;
+                const float ts = (float)grid_at_c(c, si);
+                th = (ts - c.tprev) / (c.tnext - c.tprev);
+                fl = 1 | ((si >= c.lfp_from && si < c.lfp_to) ? 2 : 0) | ((si == c.n - 1) ? 4 : 0);
+            }
+            s_theta[tid][k] = th;
+            s_rflag[tid][k] = fl;
+        }
+    }
+    lds_barrier();
+    float th[RCX][8];
+    int fl[8];
+    int anyl = 0;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        const int e = mfma_env(q, lane);
+        int f = 0;
+#pragma unroll
+        for (int k = 0; k < RCX; ++k) {
+            th[k][q] = s_theta[e][k];
+            f |= s_rflag[e][k] << (3 * k);
+        }
+        fl[q] = f;
+        anyl |= f & kLfp;
+    }
+    float pn[RCX][8];
+    double pg[RCX][8];
+#pragma unroll
+    for (int k = 0; k < RCX; ++k)
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            pn[k][q] = 0.0f;
+            pg[k][q] = 0.0;
+        }
+    // identical in every wave: each wave holds all 16 envs
+    const int anyw = __any(anyl) ? (anyl | __shfl_xor(anyl, 32, 64)) : 0;
+    // rows that feed neither an LFP sample nor the final state (the first
+    // 3999 - W saves of the reset transient) need no evaluation at all
+    const int flor = fl[0] | fl[1] | fl[2] | fl[3] | fl[4] | fl[5] | fl[6] | fl[7];
+    const bool eval_rows = __any(flor & kEval);  // LFP or final-row bits of any round
+#pragma unroll 1
+    for (int t = 0; t < (eval_rows ? TPW : 0); ++t) {
+        const int i = 32 * (wave * TPW + t) + (lane & 31);
+        float ca[8], cb[8], cc[8], f0[8], y0[8];
+        double G[8];
+        load8(ws, SL_CA, t, ca);
+        load8(ws, SL_CB, t, cb);
+        load8(ws, SL_CC, t, cc);
+        load8(ws, SL_F0, t, f0);
+        load8(ws, SL_Y0, t, y0);
+        if (gauss) {
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                int env = env_base + mfma_env(q, lane);
+                env = env < p.B ? env : p.B - 1;
+                G[q] = p.g_rec[(size_t)env * NG + col0 + i];
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < RCX; ++k) {
+            if (k >= nk) break;  // wave-uniform: past every env's last save of this step
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                const int f = fl[q] >> (3 * k);
+                if (!(f & 1)) continue;
+                const float k0 = h[q] * f0[q];
+                const float x = th[k][q];
+                float v = ca[q] * x + cb[q];
+                v = v * x + cc[q];
+                v = v * x + k0;
+                v = v * x + y0[q];
+                if (f & 2) {
+                    const float cr = kdm_cosf(v);
+                    pn[k][q] = pn[k][q] + cr;
+                    if (gauss) pg[k][q] = pg[k][q] + (double)cr * G[q];
+                }
+                const int env = env_base + mfma_env(q, lane);
+                if ((f & 4) && env < p.B) p.y[(size_t)env * NG + col0 + i] = v;
+            }
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < RCX; ++k) {
+        if (__any((anyl >> (3 * k)) & 2)) {
+            rm_publish(pn[k], k);
+            if (gauss) rm_publish_d(pg[k], k);
+        }
+    }
+    (void)anyw;
+    lds_barrier();
+    float ltot[RCX];
+    double ltot_d[RCX];
+#pragma unroll
+    for (int k = 0; k < RCX; ++k) {
+        ltot[k] = 0.0f;
+        ltot_d[k] = 0.0;
+        if (tid < E_WG && (s_rflag[tid][k] & 2)) {
+            ltot[k] = rm_total(tid, k);
+            if (gauss) ltot_d[k] = rm_total_d(tid, k);
+        }
+    }
+    if constexpr (XL) {
+        if (__builtin_amdgcn_readfirstlane(anyw) & kLfp) group_sum<RCX>(p, pt, ltot, ltot_d, RCX, gauss);
+    }
+    if (tid < E_WG) {
+        const CtlE& c = s_ctl[tid];
+        for (int k = 0; k < RCX; ++k) {
+            if (!(s_rflag[tid][k] & 2)) continue;
+            const int si = c.si + r0 + k;
+            const float ln = ltot[k] / (float)NG;
+            const double lr = gauss ? 0.0 + ltot_d[k] / (double)NG : (double)ln;
+            const int pos = si - c.lfp_from + c.pos0;
+            if (to_ring) {
+                if (!XL || pt.part == 0) p.ring[(size_t)(env_base + tid) * p.W + pos] = lr;
+            } else {
+                s_smp_n[tid][pos] = ln;
+                s_smp_r[tid][pos] = lr;
+            }
+        }
+    }
+    lds_barrier();
+}
+
 template <int TPW, bool XL>
 __device__ __forceinline__ void post_step(const DevParams& p, const Slot& ws, int env_base, bool to_ring, Part& pt
                                           STAMP_PARAMS) {
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, tid = threadIdx.x;
+    const int lane = threadIdx.x & 63, tid = threadIdx.x;
     const int NG = XL ? __builtin_amdgcn_readfirstlane(pt.ng) : TPW * 256;   // oscillators per env
-    const int col0 = XL ? __builtin_amdgcn_readfirstlane(pt.col0) : 0;       // this workgroup's first oscillator
     float h[8];
 #pragma unroll
     for (int q = 0; q < 8; ++q) h[q] = s_ctl[mfma_env(q, lane)].h;
@@ -829,137 +973,16 @@ __device__ __forceinline__ void post_step(const DevParams& p, const Slot& ws, in
     lds_barrier();
     STAMP(7);
     const int nrounds = s_maxsave;
-    // (3) saves: RC rounds (save indices) per pass over the records, all envs
-    // in parallel; one RM reduction per round and LFP kind.
+    // (3) saves: up to RCX rounds (save indices) per pass over the records,
+    // all envs in parallel; one RM reduction per round and LFP kind
     const bool gauss = p.rec_kernel == KURA_REC_GAUSSIAN;
+    if (XL || gauss) {
 #pragma unroll 1
-    for (int r0 = 0; r0 < nrounds; r0 += RC) {
-        if (tid < E_WG) {
-            const CtlE& c = s_ctl[tid];
-            for (int k = 0; k < RC; ++k) {
-                const int r = r0 + k;
-                int fl = 0;
-                float th = 0.0f;
-                if (r < c.nsave) {
-                    const int si = c.si + r;
-                    const float ts = (float)grid_at_c(c, si);
-                    th = (ts - c.tprev) / (c.tnext - c.tprev);
-                    fl = 1 | ((si >= c.lfp_from && si < c.lfp_to) ? 2 : 0) | ((si == c.n - 1) ? 4 : 0);
-                }
-                s_theta[tid][k] = th;
-                s_rflag[tid][k] = fl;
-            }
-        }
-        lds_barrier();
-        float th[RC][8];
-        int fl[8];
-        int anyl = 0;
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-            const int e = mfma_env(q, lane);
-            int f = 0;
-#pragma unroll
-            for (int k = 0; k < RC; ++k) {
-                th[k][q] = s_theta[e][k];
-                f |= s_rflag[e][k] << (3 * k);
-            }
-            fl[q] = f;
-            anyl |= f & 02222;
-        }
-        float pn[RC][8];
-        double pg[RC][8];
-#pragma unroll
-        for (int k = 0; k < RC; ++k)
-#pragma unroll
-            for (int q = 0; q < 8; ++q) {
-                pn[k][q] = 0.0f;
-                pg[k][q] = 0.0;
-            }
-        // identical in every wave: each wave holds all 16 envs
-        const int anyw = __any(anyl) ? (anyl | __shfl_xor(anyl, 32, 64)) : 0;
-        // rows that feed neither an LFP sample nor the final state (the first
-        // 3999 - W saves of the reset transient) need no evaluation at all
-        const int flor = fl[0] | fl[1] | fl[2] | fl[3] | fl[4] | fl[5] | fl[6] | fl[7];
-        const bool eval_rows = __any(flor & 06666);  // LFP or final-row bits of any round
+        for (int r0 = 0; r0 < nrounds; r0 += RC) save_pass<TPW, XL, RC>(p, ws, env_base, to_ring, pt, h, r0, nrounds, gauss);
+    } else {
 #pragma unroll 1
-        for (int t = 0; t < (eval_rows ? TPW : 0); ++t) {
-            const int i = 32 * (wave * TPW + t) + (lane & 31);
-            float ca[8], cb[8], cc[8], f0[8], y0[8];
-            double G[8];
-            load8(ws, SL_CA, t, ca);
-            load8(ws, SL_CB, t, cb);
-            load8(ws, SL_CC, t, cc);
-            load8(ws, SL_F0, t, f0);
-            load8(ws, SL_Y0, t, y0);
-            if (gauss) {
-#pragma unroll
-                for (int q = 0; q < 8; ++q) {
-                    int env = env_base + mfma_env(q, lane);
-                    env = env < p.B ? env : p.B - 1;
-                    G[q] = p.g_rec[(size_t)env * NG + col0 + i];
-                }
-            }
-#pragma unroll
-            for (int k = 0; k < RC; ++k)
-#pragma unroll
-                for (int q = 0; q < 8; ++q) {
-                    const int f = fl[q] >> (3 * k);
-                    if (!(f & 1)) continue;
-                    const float k0 = h[q] * f0[q];
-                    const float x = th[k][q];
-                    float v = ca[q] * x + cb[q];
-                    v = v * x + cc[q];
-                    v = v * x + k0;
-                    v = v * x + y0[q];
-                    if (f & 2) {
-                        const float cr = kdm_cosf(v);
-                        pn[k][q] = pn[k][q] + cr;
-                        if (gauss) pg[k][q] = pg[k][q] + (double)cr * G[q];
-                    }
-                    const int env = env_base + mfma_env(q, lane);
-                    if ((f & 4) && env < p.B) p.y[(size_t)env * NG + col0 + i] = v;
-                }
-        }
-#pragma unroll
-        for (int k = 0; k < RC; ++k) {
-            if (__any((anyl >> (3 * k)) & 2)) {
-                rm_publish(pn[k], k);
-                if (gauss) rm_publish_d(pg[k], k);
-            }
-        }
-        (void)anyw;
-        lds_barrier();
-        float ltot[RC];
-        double ltot_d[RC];
-#pragma unroll
-        for (int k = 0; k < RC; ++k) {
-            ltot[k] = 0.0f;
-            ltot_d[k] = 0.0;
-            if (tid < E_WG && (s_rflag[tid][k] & 2)) {
-                ltot[k] = rm_total(tid, k);
-                if (gauss) ltot_d[k] = rm_total_d(tid, k);
-            }
-        }
-        if constexpr (XL) {
-            if (__builtin_amdgcn_readfirstlane(anyw) & 02222) group_sum<RC>(p, pt, ltot, ltot_d, RC, gauss);
-        }
-        if (tid < E_WG) {
-            const CtlE& c = s_ctl[tid];
-            for (int k = 0; k < RC; ++k) {
-                if (!(s_rflag[tid][k] & 2)) continue;
-                const int si = c.si + r0 + k;
-                const float ln = ltot[k] / (float)NG;
-                const double lr = gauss ? 0.0 + ltot_d[k] / (double)NG : (double)ln;
-                const int pos = si - c.lfp_from + c.pos0;
-                if (to_ring) {
-                    if (!XL || pt.part == 0) p.ring[(size_t)(env_base + tid) * p.W + pos] = lr;
-                } else {
-                    s_smp_n[tid][pos] = ln;
-                    s_smp_r[tid][pos] = lr;
-                }
-            }
-        }
-        lds_barrier();
+        for (int r0 = 0; r0 < nrounds; r0 += RC_N)
+            save_pass<TPW, XL, RC_N>(p, ws, env_base, to_ring, pt, h, r0, nrounds, false);
     }
     STAMP(8);
     // (4) accepted envs: y0 <- y1, f0 <- f6 (FSAL)
