@@ -107,18 +107,20 @@ def pmc_traffic(N, B):
     passes (tools/rocprof_run.sh + tools/summarize_rocprof.py: FETCH_SIZE x2 +
     WRITE_SIZE, the same bench command).  PMC counters cannot be read from
     inside this process, so the latest committed summary for this exact
-    workload is quoted; None when there is none."""
+    workload is quoted, with the effective clock of its GRBM_GUI_ACTIVE pass;
+    None when there is none."""
     path = os.path.join(ROOT, "profiles", "latest_rocprof.json")
     try:
         with open(path) as f:
             d = json.load(f)
         wl = d["bench_under_trace"]["config"]["workload"]
         if f"N={N} " not in wl or f"x {B} envs" not in wl:
-            return None, None
+            return None, None, None
         k = d["kernels"][kernel_name(N)]
-        return k["traffic_bytes_per_dispatch"], f"profiles/latest_rocprof.json ({d['source']}): FETCH_SIZE*2 + WRITE_SIZE"
+        return (k["traffic_bytes_per_dispatch"], f"profiles/latest_rocprof.json ({d['source']}): FETCH_SIZE*2 + WRITE_SIZE",
+                k.get("effective_clock_ghz"))
     except (OSError, KeyError, ValueError):
-        return None, None
+        return None, None, None
 
 
 def main():
@@ -202,7 +204,7 @@ def main():
         # window r/w (f64 ring + f32 obs), outputs; alpha once per launch
         bytes_env = 8 * N + 4 * N + 8 * cfg.n_elec * N + 8 * max(cfg.n_rec, 0) * N + (8 + 8 + 4) * cfg.window + 64
         bytes_launch = B * bytes_env + 4 * N * N
-        traffic, traffic_src = pmc_traffic(N, B)
+        traffic, traffic_src, clock_ghz = pmc_traffic(N, B)
         out = {
             "metric": f"env steps/sec (whole node), N={N} osc x {B} envs per GPU",
             "value": value,
@@ -230,6 +232,11 @@ def main():
             "extra": {"rhs_sweeps_per_env_step": useful_rhs / B, "dopri_steps_attempted": steps_attempted,
                       "rejected": rejected, "lockstep_efficiency": lockstep_eff,
                       "executed_frac": (16.0 * wg_sweeps * 4.0 * N * N / avg_kernel_s / 1e12) / PEAK_FP32_TFLOPS, "phase_sweeps_per_s": world * useful_rhs / avg_kernel_s,
+                      # the chip holds its clock below 2.4 GHz under this kernel (DVFS): effective clock from the
+                      # committed GRBM_GUI_ACTIVE pass (tools/rocprof_run.sh) and the FP32 MFMA peak at that clock
+                      "effective_clock_ghz": clock_ghz,
+                      "frac_of_peak_at_effective_clock": (achieved_tf / (PEAK_FP32_TFLOPS * clock_ghz / 2.4)
+                                                          if clock_ghz else None),
                       "reset_ms": t_reset * 1e3, "reset_rhs_max": int(reset_stats[0]),
                       "host_setup_s": t_setup},
         }

@@ -38,10 +38,16 @@ __global__ __launch_bounds__(NTHREADS) void wave_gemm_kernel(const float* alpha_
         sum = x;
         if ((threadIdx.x & 63) == 0) out[256 * NTHREADS + blockIdx.x * 8 + wave] = (float)(t1 - t0);
     } else if (MODE == 0 || (MODE != 3 && wave < 4)) {
+        const unsigned long long c0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
         for (int r = 0; r < reps; ++r) {
             floatx16 acc[4];
             coupling_gemm<4>(Xs, alpha_sw, acc);
             for (int t = 0; t < 4; ++t) sum += acc[t][0] + acc[t][15];
+        }
+        const unsigned long long c1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+        if (threadIdx.x == 0) {  // shader clock during the GEMM: s_memtime ticks per 100 MHz s_memrealtime tick
+            out[256 * NTHREADS + 256 * 8 + 2 * blockIdx.x] = (float)(c1 - c0);
+            out[256 * NTHREADS + 256 * 8 + 2 * blockIdx.x + 1] = (float)(r1 - r0);
         }
     }
     out[blockIdx.x * NTHREADS + threadIdx.x] = sum;
@@ -73,7 +79,12 @@ static void run(const char* name, const float* dA, float* dO) {
         printf("%-40s %8.3f ms  VALU stream: %.0f cycles per wave\n", name, ms, c / 1024);
         return;
     }
+    std::vector<float> hc(512);
+    (void)hipMemcpy(hc.data(), dO + 256 * NTHREADS + 256 * 8, hc.size() * 4, hipMemcpyDeviceToHost);
+    double cyc = 0, rt = 0;
+    for (int b = 0; b < 256; ++b) cyc += hc[2 * b], rt += hc[2 * b + 1];
     const int waves = MODE == 0 ? 8 : 4;
+    printf("%-40s shader clock during the GEMM: %.2f GHz\n", name, cyc / rt * 0.1);
     // per active wave per rep: 32 rows x (4 tiles x 32 cols) x N x 2 flop
     const double flop = (double)nwg * waves * reps * 32.0 * 128.0 * N * 2.0;
     printf("%-40s %8.3f ms  %6.1f TFLOP/s\n", name, ms, flop / (ms * 1e-3) / 1e12);
@@ -85,7 +96,7 @@ int main() {
     for (size_t i = 0; i < h.size(); ++i) h[i] = 0.35f + 0.65f * (float)((i * 2654435761u) % 1000) / 1000.0f;
     float *dA, *dO;
     (void)hipMalloc(&dA, h.size() * 4);
-    (void)hipMalloc(&dO, 256 * NTHREADS * 4 + 256 * 8 * 4);
+    (void)hipMalloc(&dO, 256 * NTHREADS * 4 + 256 * 8 * 4 + 512 * 4);
     (void)hipMemcpy(dA, h.data(), h.size() * 4, hipMemcpyHostToDevice);
     run<0>("8 waves, GEMM", dA, dO);
     run<1>("waves 0-3 only, GEMM", dA, dO);

@@ -40,6 +40,20 @@ def main(src, dst):
                 d = out["kernels"].setdefault(k, {})
                 d[counter.lower() + "_bytes_per_dispatch"] = scale * 1024.0 * sum(v) / len(v)
                 d[counter.lower() + "_dispatches"] = len(v)
+    # effective shader clock: GRBM_GUI_ACTIVE (summed over the 8 XCDs) / 8 / dispatch time
+    clk = os.path.join(src, "clock", "run_counter_collection.csv")
+    if os.path.exists(clk):
+        per = {}
+        with open(clk) as f:
+            for r in csv.DictReader(f):
+                if r["Counter_Name"] != "GRBM_GUI_ACTIVE":
+                    continue
+                ns = float(r["End_Timestamp"]) - float(r["Start_Timestamp"])
+                if ns > 0:
+                    per.setdefault(_kname(r["Kernel_Name"]), []).append(float(r["Counter_Value"]) / 8.0 / ns)
+        for k, v in per.items():
+            if k.startswith("kura_"):
+                out["kernels"].setdefault(k, {})["effective_clock_ghz"] = sum(v) / len(v)
     for k, d in out["kernels"].items():
         if "fetch_size_bytes_per_dispatch" in d and "write_size_bytes_per_dispatch" in d:
             d["traffic_bytes_per_dispatch"] = d["fetch_size_bytes_per_dispatch"] + d["write_size_bytes_per_dispatch"]
