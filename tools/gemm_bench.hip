@@ -138,11 +138,28 @@ __device__ __forceinline__ void gemm_ring_after(const float* Xs, const float* al
     }
 }
 
+// operand values: low-entropy (the original bench) or random in [-1, 1] like
+// the sin/cos images (RANDOM_OPERANDS=1); the chip's clock under load depends
+// on the data (MI355X_MICROARCH.md, 'DVFS give-back')
+#ifndef RANDOM_OPERANDS
+#define RANDOM_OPERANDS 1
+#endif
+__device__ __forceinline__ float operand(int i, int b) {
+    if (RANDOM_OPERANDS) {
+        unsigned h = (unsigned)i * 2654435761u + (unsigned)b * 40503u;
+        h ^= h >> 15;
+        h *= 2246822519u;
+        h ^= h >> 13;
+        return (float)(h & 0xffff) / 32768.0f - 1.0f;
+    }
+    return 1e-3f * (float)((i * 7 + b) & 15);
+}
+
 template <int V, int TPW, int SCHED_>
 __global__ __launch_bounds__(NTHREADS) void gemm_kernel(const float* alpha_sw, float* out, int reps) {
     extern __shared__ float Xs[];
     constexpr int N = TPW * 256;
-    for (int i = threadIdx.x; i < xs_floats(N); i += blockDim.x) Xs[i] = 1e-3f * (float)((i * 7 + blockIdx.x) & 15);
+    for (int i = threadIdx.x; i < xs_floats(N); i += blockDim.x) Xs[i] = operand(i, blockIdx.x);
     __syncthreads();
     float sink = 0.0f;
     for (int r = 0; r < reps; ++r) {
@@ -202,7 +219,7 @@ __global__ __launch_bounds__(NTHREADS) void gemm16_kernel(const float* alpha_sw,
     extern __shared__ float Xs[];
     constexpr int N = 1024, NKB = N / 16;  // 16-k blocks
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, grp = wave >> 2, wg = wave & 3;
-    for (int i = threadIdx.x; i < 2 * NKB * 64 * 4; i += blockDim.x) Xs[i] = 1e-3f * (float)((i * 7 + blockIdx.x) & 15);
+    for (int i = threadIdx.x; i < 2 * NKB * 64 * 4; i += blockDim.x) Xs[i] = operand(i, blockIdx.x);
     __syncthreads();
     const floatx4* xa = reinterpret_cast<const floatx4*>(Xs) + grp * NKB * 64 + lane;
     // B tiles: [tile 0..63][kb 0..63][lane] float4; wave's tiles = 16*wg .. 16*wg+15
@@ -310,7 +327,8 @@ int main() {
     hipMalloc(&dA, (size_t)N * N * 4);
     hipMalloc(&dO, (size_t)nwg * NTHREADS * 4);
     std::vector<float> h((size_t)N * N);
-    for (size_t i = 0; i < h.size(); ++i) h[i] = 1e-3f * (float)(i % 97);
+    for (size_t i = 0; i < h.size(); ++i)
+        h[i] = RANDOM_OPERANDS ? 0.35f + 0.65f * (float)((i * 2654435761u) % 1000) / 1000.0f : 1e-3f * (float)(i % 97);
     hipMemcpy(dA, h.data(), h.size() * 4, hipMemcpyHostToDevice);
     printf("{");
     probe16();
