@@ -37,7 +37,7 @@ def distance_matrix(coords: np.ndarray) -> np.ndarray:
     as ((x^2 + y^2) + z^2); the BLAS dot of this container fuses the adds, so
     entries can differ by 1 ulp of float64 -- the float32 coupling uploaded to
     the device (jnp.array(alpha) with x64 off) is identical
-    (tests/test_golden_setup.py).
+    (tests/test_golden_reference.py).
     """
     c = np.asarray(coords, dtype=np.float64)
     d = c[:, None, :] - c[None, :, :]
