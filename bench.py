@@ -67,13 +67,10 @@ def build_shard(args, rank):
     return cfg, shared["alpha"].astype(np.float32), omega, g_stim, g_rec, theta0, ctab, stab, shared["gain"]
 
 
-def cpu_baseline(args, cfg, alpha, omega, g_stim, g_rec, theta0, ctab, stab, gain):
-    """The oracle (CPU restatement of step()) on this host's cores, bounded sample."""
+def _time_oracle(args, cfg, alpha, omega, g_stim, g_rec, theta0, ctab, stab, gain, nb, seconds):
+    """Steps/s of the oracle stepping nb envs (one env per OpenMP thread) for ~seconds after reset."""
     from oracle import kura_oracle as ko
     import copy
-    ncores = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
-    nthreads = int(os.environ.get("OMP_NUM_THREADS", ncores))
-    nb = max(1, min(nthreads, cfg.n_envs))
     c = copy.copy(cfg)
     c.n_envs = nb
     o = ko.Oracle(c, alpha)
@@ -88,13 +85,27 @@ def cpu_baseline(args, cfg, alpha, omega, g_stim, g_rec, theta0, ctab, stab, gai
         o.step(rng.uniform(-1, 1, (nb, c.n_elec)).astype(np.float32))
         k += 1
         el = time.perf_counter() - t0
-        if el >= args.cpu_seconds:
+        if el >= seconds:
             break
     o.close()
-    return {"value": nb * k / el, "unit": "env-steps/s", "cores": nthreads, "kind": "port",
+    return nb * k / el, k, el
+
+
+def cpu_baseline(args, cfg, alpha, omega, g_stim, g_rec, theta0, ctab, stab, gain):
+    """The oracle (CPU restatement of step()) on this host's cores, bounded sample:
+    all cores (one env per OpenMP thread) and, beside it, one core (one env)."""
+    ncores = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    nthreads = int(os.environ.get("OMP_NUM_THREADS", ncores))
+    nb = max(1, min(nthreads, cfg.n_envs))
+    arrs = (args, cfg, alpha, omega, g_stim, g_rec, theta0, ctab, stab, gain)
+    v, k, el = _time_oracle(*arrs, nb, args.cpu_seconds)
+    v1, k1, el1 = _time_oracle(*arrs, 1, max(1.0, args.cpu_seconds / 3))
+    return {"value": v, "unit": "env-steps/s", "cores": nthreads, "kind": "port",
             "sample": f"oracle/kura_oracle.c (CPU restatement of step(), bit-exact twin of the HIP path), "
                       f"{args.config} N={cfg.n_osc}, {nb} envs x {k} steps after reset, {el:.1f} s, "
-                      f"OpenMP {nthreads} threads (one env per thread)"}
+                      f"OpenMP {nthreads} threads (one env per thread)",
+            "single_core_value": v1,
+            "single_core_sample": f"1 env x {k1} steps, {el1:.1f} s, one thread"}
 
 
 def kernel_name(N):
