@@ -1167,25 +1167,6 @@ __device__ __forceinline__ double window_dot(const double (&x)[WPL], const doubl
     return wave_sum_f64(a);
 }
 
-// R64 order replayed serially by one lane (used where a single lane owns the
-// whole vector, e.g. the R2 filter output).
-__device__ double serial_r64_f64(const double* v, int n) {
-    double part[64];
-    for (int l = 0; l < 64; ++l) {
-        double a = 0.0;
-        for (int i = l; i < n; i += 64) a = a + v[i];
-        part[l] = a;
-    }
-    for (int o = 32; o >= 1; o >>= 1)
-        for (int l = 0; l < 64; ++l)
-            if (!(l & o)) {
-                const double v = part[l] + part[l ^ o];  // == part[l^o] + part[l]
-                part[l] = v;
-                part[l ^ o] = v;
-            }
-    return part[0];
-}
-
 // Window accessor for the serial filter: x[i] (oldest first) is either an
 // untouched slot of the ring or one of the S new samples held in LDS.
 struct WinView {
@@ -1203,32 +1184,64 @@ struct WinView {
     }
 };
 
-// R2 = -1e3 (filtfilt(x)[-1] - mean(filtfilt(x)))^2 - 1e-2|u0|, computed by
-// lane 0 (scipy lfilter DF2T order, no contraction; oracle filtfilt_last_dev).
-__device__ double filtfilt_last_dev(const DevParams& p, const WinView& xv, double* ext, double* tmp) {
+// R2 = -1e3 (filtfilt(x)[-1] - mean(filtfilt(x)))^2 - 1e-2|u0|: scipy
+// filtfilt (odd extension of padlen samples, DF2T lfilter with lfilter_zi
+// scaled by each pass's first input), oracle filtfilt_last.  Called by the
+// whole wave.  The recursion is serial, so it walks 64 samples at a time:
+// the block is loaded lane-parallel, each sample is taken in order with
+// readlane (the filter state is wave-uniform), the outputs are gathered with
+// a lane select and stored lane-parallel -- the same operations in the same
+// order as the oracle, without a memory round trip per sample.  The mean is
+// the R64 reduction (lane partials in index order, xor butterfly).
+__device__ __forceinline__ double readlane_f64(double v, int j) {
+    const uint64_t u = __builtin_bit_cast(uint64_t, v);
+    const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)u, j);
+    const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(u >> 32), j);
+    return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+__device__ double filtfilt_last_wave(const DevParams& p, const WinView& xv, double* ext, double* tmp) {
+    const int lane = threadIdx.x & 63;
     const int W = p.W, P = p.padlen, L = W + 2 * P;
     const double x0 = xv.at(0), xl = xv.at(W - 1);
-    for (int i = 0; i < P; ++i) ext[i] = 2.0 * x0 - xv.at(P - i);
-    for (int i = 0; i < W; ++i) ext[P + i] = xv.at(i);
-    for (int i = 0; i < P; ++i) ext[P + W + i] = 2.0 * xl - xv.at(W - 2 - i);
+    for (int k = lane; k < L; k += 64) {
+        double v;
+        if (k < P) v = 2.0 * x0 - xv.at(P - k);
+        else if (k < P + W) v = xv.at(k - P);
+        else v = 2.0 * xl - xv.at(W - 2 - (k - P - W));
+        ext[k] = v;
+    }
+    __threadfence_block();  // this wave's stores before its lanes read each other's elements
+    const double b0 = p.bw_b[0], b1 = p.bw_b[1], b2 = p.bw_b[2], b3 = p.bw_b[3], b4 = p.bw_b[4];
+    const double a1 = p.bw_a[1], a2 = p.bw_a[2], a3 = p.bw_a[3], a4 = p.bw_a[4];
     for (int pass = 0; pass < 2; ++pass) {
         const double e0 = ext[0];
         double z0 = p.bw_zi[0] * e0, z1 = p.bw_zi[1] * e0, z2 = p.bw_zi[2] * e0, z3 = p.bw_zi[3] * e0;
-        for (int k = 0; k < L; ++k) {
-            const double xn = ext[k];
-            const double yn = z0 + p.bw_b[0] * xn;
-            z0 = (z1 + xn * p.bw_b[1]) - yn * p.bw_a[1];
-            z1 = (z2 + xn * p.bw_b[2]) - yn * p.bw_a[2];
-            z2 = (z3 + xn * p.bw_b[3]) - yn * p.bw_a[3];
-            z3 = xn * p.bw_b[4] - yn * p.bw_a[4];
-            tmp[k] = yn;
+        for (int k0 = 0; k0 < L; k0 += 64) {
+            const int nb = L - k0 < 64 ? L - k0 : 64;
+            const double vin = k0 + lane < L ? ext[k0 + lane] : 0.0;
+            double vout = 0.0;
+            for (int j = 0; j < nb; ++j) {
+                const double xn = readlane_f64(vin, j);
+                const double yn = z0 + b0 * xn;
+                z0 = (z1 + xn * b1) - yn * a1;
+                z1 = (z2 + xn * b2) - yn * a2;
+                z2 = (z3 + xn * b3) - yn * a3;
+                z3 = xn * b4 - yn * a4;
+                vout = lane == j ? yn : vout;
+            }
+            if (k0 + lane < L) tmp[k0 + lane] = vout;
         }
-        if (pass == 0)
-            for (int i = 0; i < L; ++i) ext[i] = tmp[L - 1 - i];
+        __threadfence_block();
+        if (pass == 0) {
+            for (int k = lane; k < L; k += 64) ext[k] = tmp[L - 1 - k];
+            __threadfence_block();
+        }
     }
-    for (int i = 0; i < W; ++i) ext[i] = tmp[L - 1 - P - i];
-    const double mean = serial_r64_f64(ext, W) / (double)W;
-    return ext[W - 1] - mean;
+    // filtered window f[i] = tmp[L-1-P-i], i < W; f[W-1] = tmp[P]
+    double part = 0.0;
+    for (int i = lane; i < W; i += 64) part = part + tmp[L - 1 - P - i];
+    const double mean = wave_sum_f64(part) / (double)W;
+    return tmp[P] - mean;
 }
 
 // Reward of the window held in registers (R64 layout), env.py:638-688.
@@ -1236,16 +1249,11 @@ __device__ double filtfilt_last_dev(const DevParams& p, const WinView& xv, doubl
 template <int WPL>
 __device__ double reward_of(const DevParams& p, const double (&x)[WPL], double u0, const WinView& xv, double* ext,
                             double* tmp) {
-    const int lane = threadIdx.x & 63;
     const double au = fabs(u0);
     if (p.reward_kind == KURA_R_TEMP_CONST) {
-        double r = 0.0;
-        if (lane == 0) {
-            const double d = filtfilt_last_dev(p, xv, ext, tmp);
-            const double r1 = 1e3 * (d * d);
-            r = -r1 - 1e-2 * au;
-        }
-        return __shfl(r, 0, 64);
+        const double d = filtfilt_last_wave(p, xv, ext, tmp);
+        const double r1 = 1e3 * (d * d);
+        return __shfl(-r1 - 1e-2 * au, 0, 64);
     }
     double bb = 0.0;
     for (int b = 0; b < p.n_bins; ++b) {
