@@ -1199,60 +1199,97 @@ __device__ __forceinline__ double readlane_f64(double v, int j) {
     const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(u >> 32), j);
     return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
 }
-__device__ double filtfilt_last_wave(const DevParams& p, const WinView& xv, double* ext, double* tmp) {
+// NF independent windows at once (two envs of a wave): their recursions are
+// interleaved in one loop, which is bound by the latency of the dependent
+// f64 chain, not by issue.
+template <int NF>
+__device__ void filtfilt_last_wave(const DevParams& p, const WinView (&xv)[NF], double* const (&ext)[NF],
+                                   double* const (&tmp)[NF], double (&out)[NF]) {
     const int lane = threadIdx.x & 63;
     const int W = p.W, P = p.padlen, L = W + 2 * P;
-    const double x0 = xv.at(0), xl = xv.at(W - 1);
-    for (int k = lane; k < L; k += 64) {
-        double v;
-        if (k < P) v = 2.0 * x0 - xv.at(P - k);
-        else if (k < P + W) v = xv.at(k - P);
-        else v = 2.0 * xl - xv.at(W - 2 - (k - P - W));
-        ext[k] = v;
+#pragma unroll
+    for (int f = 0; f < NF; ++f) {
+        const double x0 = xv[f].at(0), xl = xv[f].at(W - 1);
+        for (int k = lane; k < L; k += 64) {
+            double v;
+            if (k < P) v = 2.0 * x0 - xv[f].at(P - k);
+            else if (k < P + W) v = xv[f].at(k - P);
+            else v = 2.0 * xl - xv[f].at(W - 2 - (k - P - W));
+            ext[f][k] = v;
+        }
     }
     __threadfence_block();  // this wave's stores before its lanes read each other's elements
     const double b0 = p.bw_b[0], b1 = p.bw_b[1], b2 = p.bw_b[2], b3 = p.bw_b[3], b4 = p.bw_b[4];
     const double a1 = p.bw_a[1], a2 = p.bw_a[2], a3 = p.bw_a[3], a4 = p.bw_a[4];
     for (int pass = 0; pass < 2; ++pass) {
-        const double e0 = ext[0];
-        double z0 = p.bw_zi[0] * e0, z1 = p.bw_zi[1] * e0, z2 = p.bw_zi[2] * e0, z3 = p.bw_zi[3] * e0;
+        double z0[NF], z1[NF], z2[NF], z3[NF];
+#pragma unroll
+        for (int f = 0; f < NF; ++f) {
+            const double e0 = ext[f][0];
+            z0[f] = p.bw_zi[0] * e0;
+            z1[f] = p.bw_zi[1] * e0;
+            z2[f] = p.bw_zi[2] * e0;
+            z3[f] = p.bw_zi[3] * e0;
+        }
         for (int k0 = 0; k0 < L; k0 += 64) {
             const int nb = L - k0 < 64 ? L - k0 : 64;
-            const double vin = k0 + lane < L ? ext[k0 + lane] : 0.0;
-            double vout = 0.0;
-            for (int j = 0; j < nb; ++j) {
-                const double xn = readlane_f64(vin, j);
-                const double yn = z0 + b0 * xn;
-                z0 = (z1 + xn * b1) - yn * a1;
-                z1 = (z2 + xn * b2) - yn * a2;
-                z2 = (z3 + xn * b3) - yn * a3;
-                z3 = xn * b4 - yn * a4;
-                vout = lane == j ? yn : vout;
+            double vin[NF], vout[NF];
+#pragma unroll
+            for (int f = 0; f < NF; ++f) {
+                vin[f] = k0 + lane < L ? ext[f][k0 + lane] : 0.0;
+                vout[f] = 0.0;
             }
-            if (k0 + lane < L) tmp[k0 + lane] = vout;
+            for (int j = 0; j < nb; ++j) {
+#pragma unroll
+                for (int f = 0; f < NF; ++f) {
+                    const double xn = readlane_f64(vin[f], j);
+                    const double yn = z0[f] + b0 * xn;
+                    z0[f] = (z1[f] + xn * b1) - yn * a1;
+                    z1[f] = (z2[f] + xn * b2) - yn * a2;
+                    z2[f] = (z3[f] + xn * b3) - yn * a3;
+                    z3[f] = xn * b4 - yn * a4;
+                    vout[f] = lane == j ? yn : vout[f];
+                }
+            }
+#pragma unroll
+            for (int f = 0; f < NF; ++f)
+                if (k0 + lane < L) tmp[f][k0 + lane] = vout[f];
         }
         __threadfence_block();
         if (pass == 0) {
-            for (int k = lane; k < L; k += 64) ext[k] = tmp[L - 1 - k];
+#pragma unroll
+            for (int f = 0; f < NF; ++f)
+                for (int k = lane; k < L; k += 64) ext[f][k] = tmp[f][L - 1 - k];
             __threadfence_block();
         }
     }
-    // filtered window f[i] = tmp[L-1-P-i], i < W; f[W-1] = tmp[P]
-    double part = 0.0;
-    for (int i = lane; i < W; i += 64) part = part + tmp[L - 1 - P - i];
-    const double mean = wave_sum_f64(part) / (double)W;
-    return tmp[P] - mean;
+    // filtered window g[i] = tmp[L-1-P-i], i < W; g[W-1] = tmp[P]
+#pragma unroll
+    for (int f = 0; f < NF; ++f) {
+        double part = 0.0;
+        for (int i = lane; i < W; i += 64) part = part + tmp[f][L - 1 - P - i];
+        const double mean = wave_sum_f64(part) / (double)W;
+        out[f] = tmp[f][P] - mean;
+    }
 }
 
 // Reward of the window held in registers (R64 layout), env.py:638-688.
 // Must be called by the whole wave (the DFT reductions shuffle).
 template <int WPL>
 __device__ double reward_of(const DevParams& p, const double (&x)[WPL], double u0, const WinView& xv, double* ext,
-                            double* tmp) {
+                            double* tmp, const double* d_pre = nullptr) {
     const double au = fabs(u0);
     if (p.reward_kind == KURA_R_TEMP_CONST) {
-        const double d = filtfilt_last_wave(p, xv, ext, tmp);
-        const double r1 = 1e3 * (d * d);
+        double d[1];
+        if (d_pre) {
+            d[0] = *d_pre;
+        } else {
+            const WinView v1[1] = {xv};
+            double* const e1[1] = {ext};
+            double* const t1[1] = {tmp};
+            filtfilt_last_wave<1>(p, v1, e1, t1, d);
+        }
+        const double r1 = 1e3 * (d[0] * d[0]);
         return __shfl(-r1 - 1e-2 * au, 0, 64);
     }
     double bb = 0.0;
@@ -1375,6 +1412,42 @@ __device__ __forceinline__ void step_pair(const DevParams& p, Part& pt, float* X
     // ---- window, reward, outputs (env.py:443-454): wave w owns envs 2w, 2w+1
     // (split groups: part 0; every part holds the same samples)
     constexpr int WPL = WPL_MAX;
+    // R2: the serial filters of the wave's two envs run interleaved, before the
+    // per-env loop (and so before the ring appends)
+    double r2d[ENVS_PER_WAVE] = {0.0, 0.0};
+    const bool r2 = p.reward_kind == KURA_R_TEMP_CONST && (!XL || pt.part == 0);
+    if (r2) {
+        WinView vv[ENVS_PER_WAVE];
+        double* ve[ENVS_PER_WAVE];
+        double* vt[ENVS_PER_WAVE];
+        bool ok[ENVS_PER_WAVE];
+#pragma unroll
+        for (int ee = 0; ee < ENVS_PER_WAVE; ++ee) {
+            const int e = wave * ENVS_PER_WAVE + ee;
+            const int env = env_base + e;
+            const int envx = env < p.B ? env : p.B - 1;  // padded slots: any valid address, never filtered
+            const int S = s_nI[e] + s_nII[e] - 1;
+            ok[ee] = env < p.B && !s_ctl[e].flags && S >= 1;
+            vv[ee] = WinView{p.ring + (size_t)envx * p.W, e, p.W, p.wpos[envx], S};
+            ve[ee] = p.scratch + (size_t)envx * 2 * (p.W + 2 * p.padlen);
+            vt[ee] = ve[ee] + (p.W + 2 * p.padlen);
+        }
+        static_assert(ENVS_PER_WAVE == 2, "the R2 pairing below assumes two envs per wave");
+        if (ok[0] && ok[1]) {
+            const WinView v2[2] = {vv[0], vv[1]};
+            double* const e2[2] = {ve[0], ve[1]};
+            double* const t2[2] = {vt[0], vt[1]};
+            filtfilt_last_wave<2>(p, v2, e2, t2, r2d);
+        } else if (ok[0] || ok[1]) {
+            const int f = ok[0] ? 0 : 1;
+            const WinView v1[1] = {vv[f]};
+            double* const e1[1] = {ve[f]};
+            double* const t1[1] = {vt[f]};
+            double d1[1];
+            filtfilt_last_wave<1>(p, v1, e1, t1, d1);
+            r2d[f] = d1[0];
+        }
+    }
 #pragma unroll 1
     for (int ee = 0; ee < ((!XL || pt.part == 0) ? ENVS_PER_WAVE : 0); ++ee) {
         const int e = wave * ENVS_PER_WAVE + ee;
@@ -1406,7 +1479,7 @@ __device__ __forceinline__ void step_pair(const DevParams& p, Part& pt, float* X
         }
         double* ext = p.scratch + (size_t)env * 2 * (W + 2 * p.padlen);
         double* tmp = ext + (W + 2 * p.padlen);
-        const double r = reward_of<WPL>(p, x, s_u[e][0], xv, ext, tmp);
+        const double r = reward_of<WPL>(p, x, s_u[e][0], xv, ext, tmp, r2 ? &r2d[ee] : nullptr);
         // ring append after every read of the old slots
         if (lane < S) {
             int k = wp0 + lane;
