@@ -400,6 +400,7 @@ __shared__ float s_theta[E_WG][RC_N];            // dense-output abscissae of th
 __shared__ int s_rflag[E_WG][RC_N];              // bit0: save row, bit1: LFP row, bit2: final row
 __shared__ double s_u[E_WG][4];                  // rescaled amplitudes (env.py:389-393)
 __shared__ int s_maxsave, s_any;
+__shared__ int s_nI[E_WG], s_nII[E_WG];          // ON / OFF grid lengths of the step (step_pair)
 
 __device__ __forceinline__ double grid_at_c(const CtlE& c, int i) {
     return i == 0 ? c.g_start : c.g_start + (double)i * c.g_delta;
@@ -1329,12 +1330,94 @@ __device__ __forceinline__ Part make_part(const DevParams& p, int pair) {
     return pt;
 }
 
+// R2 filters of the workgroup's envs (scipy filtfilt, oracle filtfilt_last),
+// same operations in the same order as filtfilt_last_wave:
+//  (A) each wave writes the odd-extended windows of its two envs to their
+//      scratch (lane-parallel);
+//  (B) wave 0 runs both recursion passes, lane e walking env e's sequence
+//      (16 chains per instruction stream instead of one), 16 samples per
+//      block of independent loads; pass 2 reads pass 1's output backwards;
+//  (C) each wave reduces the mean of its envs' filtered windows (R64 order).
+// Must be called by the whole workgroup; out[ee] = f[W-1] - mean(f) of env
+// 2*wave + ee (0 for envs without a reward).
+__device__ void r2_filters_wg(const DevParams& p, int env_base, double (&out)[ENVS_PER_WAVE]) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int W = p.W, P = p.padlen, L = W + 2 * P;
+    auto env_ok = [&](int e) {
+        const int env = env_base + e;
+        return env < p.B && !s_ctl[e].flags && (s_nI[e] + s_nII[e] - 1) >= 1;
+    };
+    auto ext_of = [&](int e) { return p.scratch + (size_t)(env_base + e) * 2 * (W + 2 * P); };
+    // (A)
+#pragma unroll 1
+    for (int ee = 0; ee < ENVS_PER_WAVE; ++ee) {
+        const int e = wave * ENVS_PER_WAVE + ee;
+        if (!env_ok(e)) continue;
+        const int env = env_base + e;
+        const WinView xv{p.ring + (size_t)env * W, e, W, p.wpos[env], s_nI[e] + s_nII[e] - 1};
+        double* ext = ext_of(e);
+        const double x0 = xv.at(0), xl = xv.at(W - 1);
+        for (int k = lane; k < L; k += 64) {
+            double v;
+            if (k < P) v = 2.0 * x0 - xv.at(P - k);
+            else if (k < P + W) v = xv.at(k - P);
+            else v = 2.0 * xl - xv.at(W - 2 - (k - P - W));
+            ext[k] = v;
+        }
+    }
+    __syncthreads();
+    // (B)
+    if (wave == 0 && lane < E_WG && env_ok(lane)) {
+        double* ext = ext_of(lane);
+        double* tmp = ext + L;
+        const double b0 = p.bw_b[0], b1 = p.bw_b[1], b2 = p.bw_b[2], b3 = p.bw_b[3], b4 = p.bw_b[4];
+        const double a1 = p.bw_a[1], a2 = p.bw_a[2], a3 = p.bw_a[3], a4 = p.bw_a[4];
+        for (int pass = 0; pass < 2; ++pass) {
+            // pass 0: ext -> tmp; pass 1: tmp read backwards -> ext
+            const double* src = pass == 0 ? ext : tmp;
+            double* dst = pass == 0 ? tmp : ext;
+            auto in = [&](int k) { return pass == 0 ? src[k] : src[L - 1 - k]; };
+            const double e0 = in(0);
+            double z0 = p.bw_zi[0] * e0, z1 = p.bw_zi[1] * e0, z2 = p.bw_zi[2] * e0, z3 = p.bw_zi[3] * e0;
+            constexpr int BLK = 16;
+            for (int k0 = 0; k0 < L; k0 += BLK) {
+                double xb[BLK];
+#pragma unroll
+                for (int i = 0; i < BLK; ++i) xb[i] = k0 + i < L ? in(k0 + i) : 0.0;
+#pragma unroll
+                for (int i = 0; i < BLK; ++i) {
+                    if (k0 + i >= L) break;
+                    const double xn = xb[i];
+                    const double yn = z0 + b0 * xn;
+                    z0 = (z1 + xn * b1) - yn * a1;
+                    z1 = (z2 + xn * b2) - yn * a2;
+                    z2 = (z3 + xn * b3) - yn * a3;
+                    z3 = xn * b4 - yn * a4;
+                    dst[k0 + i] = yn;
+                }
+            }
+        }
+    }
+    __syncthreads();
+    // (C) filtered window f[i] = y2[L-1-P-i] (y2 in ext), f[W-1] = y2[P]
+#pragma unroll
+    for (int ee = 0; ee < ENVS_PER_WAVE; ++ee) {
+        const int e = wave * ENVS_PER_WAVE + ee;
+        out[ee] = 0.0;
+        if (!env_ok(e)) continue;
+        const double* y2 = ext_of(e);
+        double part = 0.0;
+        for (int i = lane; i < W; i += 64) part = part + y2[L - 1 - P - i];
+        const double mean = wave_sum_f64(part) / (double)W;
+        out[ee] = y2[P] - mean;
+    }
+}
+
 template <int TPW, bool XL>
 __device__ __forceinline__ void step_pair(const DevParams& p, Part& pt, float* Xs, const float* __restrict__ action,
                                           float* __restrict__ obs, double* __restrict__ reward,
                                           uint8_t* __restrict__ done, float* __restrict__ lfp_true,
                                           double* __restrict__ lfp_rec, int* __restrict__ nsamp) {
-    __shared__ int s_nI[E_WG], s_nII[E_WG];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, tid = threadIdx.x;
     const int N = p.N;
     const int env_base = pt.group * E_WG;
@@ -1412,42 +1495,12 @@ __device__ __forceinline__ void step_pair(const DevParams& p, Part& pt, float* X
     // ---- window, reward, outputs (env.py:443-454): wave w owns envs 2w, 2w+1
     // (split groups: part 0; every part holds the same samples)
     constexpr int WPL = WPL_MAX;
-    // R2: the serial filters of the wave's two envs run interleaved, before the
-    // per-env loop (and so before the ring appends)
+    // R2: the serial filters of all 16 envs of the workgroup run in one wave,
+    // one lane per env (r2_filters_wg), before the per-env loop (and so before
+    // the ring appends)
     double r2d[ENVS_PER_WAVE] = {0.0, 0.0};
     const bool r2 = p.reward_kind == KURA_R_TEMP_CONST && (!XL || pt.part == 0);
-    if (r2) {
-        WinView vv[ENVS_PER_WAVE];
-        double* ve[ENVS_PER_WAVE];
-        double* vt[ENVS_PER_WAVE];
-        bool ok[ENVS_PER_WAVE];
-#pragma unroll
-        for (int ee = 0; ee < ENVS_PER_WAVE; ++ee) {
-            const int e = wave * ENVS_PER_WAVE + ee;
-            const int env = env_base + e;
-            const int envx = env < p.B ? env : p.B - 1;  // padded slots: any valid address, never filtered
-            const int S = s_nI[e] + s_nII[e] - 1;
-            ok[ee] = env < p.B && !s_ctl[e].flags && S >= 1;
-            vv[ee] = WinView{p.ring + (size_t)envx * p.W, e, p.W, p.wpos[envx], S};
-            ve[ee] = p.scratch + (size_t)envx * 2 * (p.W + 2 * p.padlen);
-            vt[ee] = ve[ee] + (p.W + 2 * p.padlen);
-        }
-        static_assert(ENVS_PER_WAVE == 2, "the R2 pairing below assumes two envs per wave");
-        if (ok[0] && ok[1]) {
-            const WinView v2[2] = {vv[0], vv[1]};
-            double* const e2[2] = {ve[0], ve[1]};
-            double* const t2[2] = {vt[0], vt[1]};
-            filtfilt_last_wave<2>(p, v2, e2, t2, r2d);
-        } else if (ok[0] || ok[1]) {
-            const int f = ok[0] ? 0 : 1;
-            const WinView v1[1] = {vv[f]};
-            double* const e1[1] = {ve[f]};
-            double* const t1[1] = {vt[f]};
-            double d1[1];
-            filtfilt_last_wave<1>(p, v1, e1, t1, d1);
-            r2d[f] = d1[0];
-        }
-    }
+    if (r2) r2_filters_wg(p, env_base, r2d);
 #pragma unroll 1
     for (int ee = 0; ee < ((!XL || pt.part == 0) ? ENVS_PER_WAVE : 0); ++ee) {
         const int e = wave * ENVS_PER_WAVE + ee;
