@@ -1379,23 +1379,35 @@ __device__ void r2_filters_wg(const DevParams& p, int env_base, double (&out)[EN
             auto in = [&](int k) { return pass == 0 ? src[k] : src[L - 1 - k]; };
             const double e0 = in(0);
             double z0 = p.bw_zi[0] * e0, z1 = p.bw_zi[1] * e0, z2 = p.bw_zi[2] * e0, z3 = p.bw_zi[3] * e0;
+            auto sample = [&](double xn) {
+                const double yn = z0 + b0 * xn;
+                z0 = (z1 + xn * b1) - yn * a1;
+                z1 = (z2 + xn * b2) - yn * a2;
+                z2 = (z3 + xn * b3) - yn * a3;
+                z3 = xn * b4 - yn * a4;
+                return yn;
+            };
+            // full blocks of BLK samples, the next block's loads in flight
+            // while this block's recursion runs; then the tail
             constexpr int BLK = 16;
-            for (int k0 = 0; k0 < L; k0 += BLK) {
-                double xb[BLK];
+            const int nfull = L / BLK;
+            double xb[BLK];
 #pragma unroll
-                for (int i = 0; i < BLK; ++i) xb[i] = k0 + i < L ? in(k0 + i) : 0.0;
+            for (int i = 0; i < BLK; ++i) xb[i] = nfull > 0 ? in(i) : 0.0;
+#pragma unroll 1
+            for (int b = 0; b < nfull; ++b) {
+                const int k0 = b * BLK;
+                const bool more = b + 1 < nfull;
+                double xp[BLK];
 #pragma unroll
-                for (int i = 0; i < BLK; ++i) {
-                    if (k0 + i >= L) break;
-                    const double xn = xb[i];
-                    const double yn = z0 + b0 * xn;
-                    z0 = (z1 + xn * b1) - yn * a1;
-                    z1 = (z2 + xn * b2) - yn * a2;
-                    z2 = (z3 + xn * b3) - yn * a3;
-                    z3 = xn * b4 - yn * a4;
-                    dst[k0 + i] = yn;
-                }
+                for (int i = 0; i < BLK; ++i) xp[i] = more ? in(k0 + BLK + i) : 0.0;
+#pragma unroll
+                for (int i = 0; i < BLK; ++i) dst[k0 + i] = sample(xb[i]);
+#pragma unroll
+                for (int i = 0; i < BLK; ++i) xb[i] = xp[i];
             }
+#pragma unroll 1
+            for (int k = nfull * BLK; k < L; ++k) dst[k] = sample(in(k));
         }
     }
     __syncthreads();
