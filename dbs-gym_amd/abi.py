@@ -96,6 +96,8 @@ _SYMBOLS = {
     "kura_psd_bbpow": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int, c_double, c_double, c_double, c_void_p,
                                c_void_p]),
     "kura_episode_bbpow": (c_int, [c_void_p, c_void_p, c_double, c_double, c_double, c_void_p, c_void_p]),
+    "kura_envelope_stats": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int, c_void_p, c_void_p]),
+    "kura_episode_envelope_stats": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p]),
     "kura_get_stats": (c_int, [c_void_p, c_void_p, c_int]),
     "kura_get_stamps": (c_int, [c_void_p, c_void_p]),
     "kura_selftest_math": (c_int, [c_void_p, c_void_p, c_void_p, c_int]),

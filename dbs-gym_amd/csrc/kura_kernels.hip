@@ -1863,4 +1863,161 @@ __global__ __launch_bounds__(NTHREADS) void kura_selftest_gemm_kernel(const floa
 }
 
 // explicit instantiations are made by the launchers in kura_capi.hip
+// ---- episode envelope statistics (aDBS_RL/agents/custom_callbacks.py:146-148)
+// log_main_metrics('per_episode', 'envelope', calc_envelope(lfp_ep)):
+// calc_envelope = |scipy.signal.hilbert(x)| (environment/utils.py:835-836),
+// then mean, std(ddof=1) and sum (custom_callbacks.py:28-31).  Hilbert as
+// scipy does it: X = fft(x), X[k] *= h[k] (h = 1 at DC and, for even n, at
+// n/2; 2 on the positive bins; 0 on the negative ones), z = ifft.  Three
+// kernels per chunk of signals, float64 throughout, direct DFT with exact
+// per-term twiddles (sincospi of (k*t mod n)/n): O(n^2) work, compute bound;
+// an evaluation-time metric, not on the step path.
+#define ENV_THREADS 256
+#define ENV_TILE 1024
+
+__device__ __forceinline__ bool env_signal(const DevParams& p, const float* sig, const int* lens, long long ld,
+                                           int j, int episode, const uint8_t* mask, int& L, const float*& x) {
+    if (episode) {
+        L = p.ep_len[j];
+        x = p.ep_lfp + (size_t)j * p.episode_cap;
+        return !(mask && !mask[j]) && L >= 1 && L <= p.episode_cap;
+    }
+    L = lens[j];
+    x = sig + (size_t)j * ld;
+    return L >= 1 && L <= ld;
+}
+
+// analytic half-spectrum h[k]*X[k], k in [0, L/2]: one thread per bin,
+// signal tiles staged through LDS (float -> double once per tile)
+__global__ __launch_bounds__(ENV_THREADS) void kura_env_fwd_kernel(DevParams p, const float* __restrict__ sig,
+                                                                   const int* __restrict__ lens, long long ld,
+                                                                   int j0, int episode,
+                                                                   const uint8_t* __restrict__ mask,
+                                                                   double* scratch, long long sld) {
+    __shared__ double s_x[ENV_TILE];
+    const int j = j0 + blockIdx.y;
+    int L;
+    const float* x;
+    if (!env_signal(p, sig, lens, ld, j, episode, mask, L, x)) return;
+    const int nb = L / 2 + 1;
+    if ((int)(blockIdx.x * ENV_THREADS) >= nb) return;  // whole block idle (uniform)
+    const int k = blockIdx.x * ENV_THREADS + threadIdx.x;
+    const bool act = k < nb;
+    const long long kk = act ? k : 0;
+    const double inv = 2.0 / (double)L;
+    double re = 0.0, im = 0.0;
+    long long m = 0;  // (k * t) mod L
+    for (int t0 = 0; t0 < L; t0 += ENV_TILE) {
+        const int cnt = L - t0 < ENV_TILE ? L - t0 : ENV_TILE;
+        __syncthreads();
+        for (int i = threadIdx.x; i < cnt; i += ENV_THREADS) s_x[i] = (double)x[t0 + i];
+        __syncthreads();
+        for (int i = 0; i < cnt; ++i) {
+            double sn, cs;
+            sincospi((double)m * inv, &sn, &cs);
+            re = fma(s_x[i], cs, re);
+            im = fma(-s_x[i], sn, im);
+            m += kk;
+            if (m >= L) m -= L;
+        }
+    }
+    if (act) {
+        const double h = (k == 0 || (L % 2 == 0 && k == L / 2)) ? 1.0 : 2.0;
+        double* X = scratch + (size_t)blockIdx.y * sld;
+        X[2 * k] = h * re;
+        X[2 * k + 1] = h * im;
+    }
+}
+
+// |z[t]| = |ifft(hX)[t]| for t in [0, L): one thread per sample, the half
+// spectrum staged through LDS
+__global__ __launch_bounds__(ENV_THREADS) void kura_env_inv_kernel(DevParams p, const float* __restrict__ sig,
+                                                                   const int* __restrict__ lens, long long ld,
+                                                                   int j0, int episode,
+                                                                   const uint8_t* __restrict__ mask,
+                                                                   double* scratch, long long sld) {
+    __shared__ double s_X[2 * (ENV_TILE / 2)];
+    const int j = j0 + blockIdx.y;
+    int L;
+    const float* x;
+    if (!env_signal(p, sig, lens, ld, j, episode, mask, L, x)) return;
+    if ((int)(blockIdx.x * ENV_THREADS) >= L) return;
+    const int nb = L / 2 + 1;
+    const int t = blockIdx.x * ENV_THREADS + threadIdx.x;
+    const bool act = t < L;
+    const long long tt = act ? t : 0;
+    const double inv = 2.0 / (double)L;
+    const double* X = scratch + (size_t)blockIdx.y * sld;
+    double re = 0.0, im = 0.0;
+    long long m = 0;  // (k * t) mod L
+    constexpr int TB = ENV_TILE / 2;
+    for (int k0 = 0; k0 < nb; k0 += TB) {
+        const int cnt = nb - k0 < TB ? nb - k0 : TB;
+        __syncthreads();
+        for (int i = threadIdx.x; i < 2 * cnt; i += ENV_THREADS) s_X[i] = X[2 * k0 + i];
+        __syncthreads();
+        for (int i = 0; i < cnt; ++i) {
+            double sn, cs;
+            sincospi((double)m * inv, &sn, &cs);
+            const double a = s_X[2 * i], b = s_X[2 * i + 1];
+            re = fma(a, cs, re);
+            re = fma(-b, sn, re);
+            im = fma(a, sn, im);
+            im = fma(b, cs, im);
+            m += tt;
+            if (m >= L) m -= L;
+        }
+    }
+    if (act) {
+        double* E = scratch + (size_t)blockIdx.y * sld + 2 * (size_t)nb;
+        E[t] = hypot(re, im) / (double)L;
+    }
+}
+
+// out[3j..3j+2] = mean, std(ddof=1), sum of the envelope (fixed-order f64
+// reductions; NaN for unselected / out-of-range signals, std NaN for L == 1)
+__global__ __launch_bounds__(ENV_THREADS) void kura_env_stats_kernel(DevParams p, const float* __restrict__ sig,
+                                                                     const int* __restrict__ lens, long long ld,
+                                                                     int j0, int episode,
+                                                                     const uint8_t* __restrict__ mask,
+                                                                     const double* scratch, long long sld,
+                                                                     double* __restrict__ out) {
+    __shared__ double s_r[ENV_THREADS];
+    const int j = j0 + blockIdx.x, tid = threadIdx.x;
+    const double qnan = __builtin_nan("");
+    int L;
+    const float* x;
+    if (!env_signal(p, sig, lens, ld, j, episode, mask, L, x)) {
+        if (tid == 0) out[3 * j] = out[3 * j + 1] = out[3 * j + 2] = qnan;
+        return;
+    }
+    const double* E = scratch + (size_t)blockIdx.x * sld + 2 * (size_t)(L / 2 + 1);
+    auto block_sum = [&](double v) {
+        s_r[tid] = v;
+        __syncthreads();
+        for (int w = ENV_THREADS / 2; w > 0; w >>= 1) {
+            if (tid < w) s_r[tid] += s_r[tid + w];
+            __syncthreads();
+        }
+        const double r = s_r[0];
+        __syncthreads();
+        return r;
+    };
+    double a = 0.0;
+    for (int t = tid; t < L; t += ENV_THREADS) a += E[t];
+    const double sum = block_sum(a);
+    const double mean = sum / (double)L;
+    double q = 0.0;
+    for (int t = tid; t < L; t += ENV_THREADS) {
+        const double d = E[t] - mean;
+        q = fma(d, d, q);
+    }
+    const double ss = block_sum(q);
+    if (tid == 0) {
+        out[3 * j] = mean;
+        out[3 * j + 1] = L > 1 ? sqrt(ss / (double)(L - 1)) : qnan;
+        out[3 * j + 2] = sum;
+    }
+}
+
 #include "kura_capi.inc"

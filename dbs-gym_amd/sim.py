@@ -176,6 +176,31 @@ class KuraSim:
                   "kura_psd_bbpow")
         return out.cpu().numpy()
 
+    def envelope_stats(self, signals) -> np.ndarray:
+        """[n, 3] mean, std(ddof=1), sum of |hilbert(x)| per float32 signal
+        (custom_callbacks.py:146-148, utils.py:835-836)."""
+        n = len(signals)
+        ld = max(1, max((len(x) for x in signals), default=1))
+        buf = np.zeros((n, ld), np.float32)
+        for j, x in enumerate(signals):
+            buf[j, :len(x)] = x
+        lens = torch.tensor([len(x) for x in signals], dtype=torch.int32, device=self.device)
+        sig = torch.from_numpy(buf).to(self.device)
+        out = torch.empty((n, 3), dtype=torch.float64, device=self.device)
+        with torch.cuda.device(self.device):
+            check(self.lib, self.lib.kura_envelope_stats(self._h, ptr(sig), ptr(lens), ld, n, ptr(out),
+                                                         self._stream()), "kura_envelope_stats")
+        return out.cpu().numpy()
+
+    def episode_envelope_stats(self, mask: torch.Tensor | None = None) -> torch.Tensor:
+        """The same statistics of each env's running episode (config.episode_cap > 0): [B, 3]."""
+        out = torch.empty((self.B, 3), dtype=torch.float64, device=self.device)
+        m = None if mask is None else mask.to(self.device, torch.uint8).contiguous()
+        with torch.cuda.device(self.device):
+            check(self.lib, self.lib.kura_episode_envelope_stats(self._h, ptr(m), ptr(out), self._stream()),
+                  "kura_episode_envelope_stats")
+        return out
+
     def episode_bbpow(self, mask: torch.Tensor | None = None, psd_dt: float = 5e-4,
                       beta=(12.5, 21.0)) -> torch.Tensor:
         """The same metric of each env's running episode (config.episode_cap > 0)."""

@@ -151,6 +151,9 @@ class KuraVectorEnv:
                 mask[idx] = 1
                 bb = self.sim.episode_bbpow(mask, self.psd_dt, self.beta_band)
                 infos["episode"]["bbpow"] = bb[torch.as_tensor(idx, device=self.device)].cpu().numpy()
+                # per_episode/envelope/{mean,std,cum} of the training callback (custom_callbacks.py:146-148)
+                ev = self.sim.episode_envelope_stats(mask)
+                infos["episode"]["envelope"] = ev[torch.as_tensor(idx, device=self.device)].cpu().numpy()
         if self.autoreset and term_host.any():
             infos["terminal_observation"] = obs[torch.as_tensor(idx, device=self.device)].clone().view(-1, 1, self.W)
             mask = torch.zeros(self.num_envs, dtype=torch.uint8)

@@ -113,6 +113,21 @@ int kura_psd_bbpow(KuraHandle* h, const float* sig, const int32_t* len, int64_t 
  * starts the next one (KuraVectorEnv does so for autoreset envs). */
 int kura_episode_bbpow(KuraHandle* h, const uint8_t* mask, double psd_dt, double beta_a, double beta_b,
                        double* out, void* stream);
+/* per-episode envelope statistics of the training callback
+ * (aDBS_RL/agents/custom_callbacks.py:146-148: log_main_metrics('per_episode',
+ * 'envelope', calc_envelope(lfp_ep)), with calc_envelope = |hilbert(x)|,
+ * environment/utils.py:835-836, and log_main_metrics = mean, std(ddof=1),
+ * sum, custom_callbacks.py:28-31) of n device signals sig[j*ld ...] of len[j]
+ * float32 samples.  out[3j..3j+2] (device f64) = mean, std, sum; NaN for
+ * len[j] outside [1, ld] (std NaN for len 1).  Float64 direct DFT (O(len^2),
+ * evaluation-time only); SciPy's hilbert of float32 input runs in complex64,
+ * so the reference agrees to ~1e-5 relative, the float64 restatement to ~1e-10. */
+int kura_envelope_stats(KuraHandle* h, const float* sig, const int32_t* len, int64_t ld, int n, double* out,
+                        void* stream);
+/* the same statistics of every env's current-episode true LFP (requires
+ * cfg.episode_cap > 0); mask[b] (device, NULL = all) selects envs; out[3b..]
+ * NaN for unselected envs.  Call it where kura_episode_bbpow is called. */
+int kura_episode_envelope_stats(KuraHandle* h, const uint8_t* mask, double* out, void* stream);
 /* per-env coupling gain float32(K_b / N) for envs [env0, env0+n) (host
  * array; each reference env has its own params_dict['K'], env.py:264).  Envs
  * not set keep the config's kn. */

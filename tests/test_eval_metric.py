@@ -72,4 +72,47 @@ def test_gpu_episode_record_metric():
     ref = kura_eval.calc_psd_for_simple_eval([np.concatenate(x) for x in lfp], 5e-4)
     got = info["episode"]["bbpow"]
     np.testing.assert_allclose(got, ref, rtol=RTOL, atol=0)
+    env_ref = kura_eval.envelope_stats([np.concatenate(x) for x in lfp])
+    np.testing.assert_allclose(info["episode"]["envelope"], env_ref, rtol=1e-9, atol=0)
     env.close()
+
+
+# ---- envelope statistics (custom_callbacks.py:146-148) -------------------
+from make_golden_envelope import edge_signals  # noqa: E402
+
+GE = np.load(os.path.join(ROOT, "tests", "golden", "reference_envelope_golden.npz"))
+ENV_REF_RTOL = 2e-5   # the reference's hilbert runs in complex64 (float32 input)
+ENV_RTOL = 1e-9       # GPU float64 direct DFT vs the float64 restatement (pocketfft)
+
+
+def _env_signals():
+    return signals() + edge_signals()
+
+
+def test_envelope_restatement_matches_reference():
+    got = kura_eval.envelope_stats(_env_signals())
+    np.testing.assert_allclose(got, GE["env_stats"], rtol=ENV_REF_RTOL, atol=1e-7, equal_nan=True)
+
+
+def test_envelope_restatement_matches_scipy_f64():
+    from scipy.signal import hilbert
+    for x in edge_signals()[1:]:
+        e = np.abs(hilbert(x.astype(np.float64)))
+        got = kura_eval.envelope_stats([x])[0]
+        np.testing.assert_allclose(got, [e.mean(), e.std(ddof=1), e.sum()], rtol=1e-12)
+
+
+@pytest.mark.gpu
+def test_gpu_envelope_stats_matches_restatement():
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    sim_mod = importlib.import_module("dbs-gym_amd.sim")
+    cfg = sim_mod.make_config(kura.reference_params("env0"), 4, reward_func="bbpow_action")
+    sim = sim_mod.KuraSim(cfg, 0)
+    sig = _env_signals()
+    got = sim.envelope_stats(sig)
+    want = kura_eval.envelope_stats(sig)
+    np.testing.assert_allclose(got, want, rtol=ENV_RTOL, atol=1e-12, equal_nan=True)
+    np.testing.assert_allclose(got, GE["env_stats"], rtol=ENV_REF_RTOL, atol=1e-7, equal_nan=True)
+    sim.close()
