@@ -1869,8 +1869,9 @@ __global__ __launch_bounds__(NTHREADS) void kura_selftest_gemm_kernel(const floa
 // then mean, std(ddof=1) and sum (custom_callbacks.py:28-31).  Hilbert as
 // scipy does it: X = fft(x), X[k] *= h[k] (h = 1 at DC and, for even n, at
 // n/2; 2 on the positive bins; 0 on the negative ones), z = ifft.  Three
-// kernels per chunk of signals, float64 throughout, direct DFT with exact
-// per-term twiddles (sincospi of (k*t mod n)/n): O(n^2) work, compute bound;
+// kernels per chunk of signals, float64 throughout, direct DFT with twiddles
+// exact (sincospi of (k*t mod n)/n) at each 1024/512-term tile start and
+// rotated inside it: O(n^2) work, compute bound;
 // an evaluation-time metric, not on the step path.
 #define ENV_THREADS 256
 #define ENV_TILE 1024
@@ -1906,19 +1907,25 @@ __global__ __launch_bounds__(ENV_THREADS) void kura_env_fwd_kernel(DevParams p, 
     const long long kk = act ? k : 0;
     const double inv = 2.0 / (double)L;
     double re = 0.0, im = 0.0;
-    long long m = 0;  // (k * t) mod L
+    double ws, wc;  // per-sample rotation e^{-2 pi i k / L}
+    sincospi((double)kk * inv, &ws, &wc);
+    ws = -ws;
     for (int t0 = 0; t0 < L; t0 += ENV_TILE) {
         const int cnt = L - t0 < ENV_TILE ? L - t0 : ENV_TILE;
         __syncthreads();
         for (int i = threadIdx.x; i < cnt; i += ENV_THREADS) s_x[i] = (double)x[t0 + i];
         __syncthreads();
+        // exact twiddle at the tile start, rotated within the tile (error
+        // growth ~ENV_TILE ulp, far inside the 1e-9 parity bar)
+        double cs, sn;
+        sincospi((double)((kk * t0) % L) * inv, &sn, &cs);
+        sn = -sn;
         for (int i = 0; i < cnt; ++i) {
-            double sn, cs;
-            sincospi((double)m * inv, &sn, &cs);
             re = fma(s_x[i], cs, re);
-            im = fma(-s_x[i], sn, im);
-            m += kk;
-            if (m >= L) m -= L;
+            im = fma(s_x[i], sn, im);
+            const double c2 = fma(cs, wc, -sn * ws);
+            sn = fma(cs, ws, sn * wc);
+            cs = c2;
         }
     }
     if (act) {
@@ -1949,23 +1956,25 @@ __global__ __launch_bounds__(ENV_THREADS) void kura_env_inv_kernel(DevParams p, 
     const double inv = 2.0 / (double)L;
     const double* X = scratch + (size_t)blockIdx.y * sld;
     double re = 0.0, im = 0.0;
-    long long m = 0;  // (k * t) mod L
+    double ws, wc;  // per-bin rotation e^{+2 pi i t / L}
+    sincospi((double)tt * inv, &ws, &wc);
     constexpr int TB = ENV_TILE / 2;
     for (int k0 = 0; k0 < nb; k0 += TB) {
         const int cnt = nb - k0 < TB ? nb - k0 : TB;
         __syncthreads();
         for (int i = threadIdx.x; i < 2 * cnt; i += ENV_THREADS) s_X[i] = X[2 * k0 + i];
         __syncthreads();
+        double cs, sn;  // exact at the tile start, rotated within it
+        sincospi((double)(((long long)k0 * tt) % L) * inv, &sn, &cs);
         for (int i = 0; i < cnt; ++i) {
-            double sn, cs;
-            sincospi((double)m * inv, &sn, &cs);
             const double a = s_X[2 * i], b = s_X[2 * i + 1];
             re = fma(a, cs, re);
             re = fma(-b, sn, re);
             im = fma(a, sn, im);
             im = fma(b, cs, im);
-            m += tt;
-            if (m >= L) m -= L;
+            const double c2 = fma(cs, wc, -sn * ws);
+            sn = fma(cs, ws, sn * wc);
+            cs = c2;
         }
     }
     if (act) {
