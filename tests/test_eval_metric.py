@@ -116,3 +116,20 @@ def test_gpu_envelope_stats_matches_restatement():
     np.testing.assert_allclose(got, want, rtol=ENV_RTOL, atol=1e-12, equal_nan=True)
     np.testing.assert_allclose(got, GE["env_stats"], rtol=ENV_REF_RTOL, atol=1e-7, equal_nan=True)
     sim.close()
+
+
+@pytest.mark.gpu
+def test_gpu_callback_log_psd_band():
+    """The training callback's log_psd band power (custom_callbacks.py:38-67:
+    the same filter/PSD/smoothing, band 12.5 < f < 33.5) through kura_psd_bbpow."""
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    sim_mod = importlib.import_module("dbs-gym_amd.sim")
+    cfg = sim_mod.make_config(kura.reference_params("env0"), 4, reward_func="bbpow_action")
+    sim = sim_mod.KuraSim(cfg, 0)
+    sig = signals()
+    got = sim.psd_bbpow(sig, psd_dt=float(G["psd_dt"]), beta=(12.5, 33.5))
+    want = kura_eval.calc_psd_for_simple_eval(sig, float(G["psd_dt"]), 12.5, 33.5)
+    np.testing.assert_allclose(got, want, rtol=RTOL, atol=0)
+    sim.close()
