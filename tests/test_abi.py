@@ -75,3 +75,15 @@ int main(void) {
     for f, off in got.items():
         if f != "sizeof":
             assert getattr(abi.KuraConfig, f).offset == int(off), f
+
+
+def test_metric_entry_points_reject_null_handle():
+    """Argument checks run before any HIP call: a null handle is
+    KURA_E_INVALID (-1) for the episode-metric entry points, no GPU needed."""
+    if not os.path.exists(abi.LIB_PATH):
+        pytest.skip("libkura.so not built")
+    lib = abi.load_library()
+    assert lib.kura_envelope_stats(None, None, None, 16, 1, None, None) == -1
+    assert lib.kura_episode_envelope_stats(None, None, None, None) == -1
+    assert lib.kura_psd_bbpow(None, None, None, 16, 1, 5e-4, 12.5, 21.0, None, None) == -1
+    assert lib.kura_episode_bbpow(None, None, 5e-4, 12.5, 21.0, None, None) == -1
