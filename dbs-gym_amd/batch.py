@@ -17,10 +17,18 @@ from .configs import STIM_REC_LOCUS
 
 
 class EnvHost:
-    def __init__(self, params: dict):
+    """``rs``: the RandomState standing in for the reference's process-global
+    NumPy RNG.  By default each env owns one; pass a shared one to replay a
+    driver that constructs several envs in one process (it is reseeded here
+    with this env's rand_seed, as SpatialKuramoto.__init__ does, env.py:291)."""
+
+    def __init__(self, params: dict, rs: np.random.RandomState | None = None):
         p = params
         self.p = p
-        self.rs = np.random.RandomState(p["rand_seed"])                       # env.py:291
+        if rs is None:
+            rs = np.random.RandomState()
+        rs.seed(p["rand_seed"])                                                # env.py:291
+        self.rs = rs
         self.reset_count = -1
         self.N = int(p["num_oscillators"])
         self.grid = np.asarray(p["neur_grid"])
@@ -35,6 +43,16 @@ class EnvHost:
             self.elec_drift_episode = p["electrode_drift_freq"]
             self.elec_encaps_episode = p["encapsulation_drift_freq"]
             self.encaps_precent = p["encapsulation_percent"]
+            # env.py:509 adds encapsulation_percent to the conduct modifier as
+            # is (+2 on 0.1: SURVEY.md Appendix C3).  "relative" reads the
+            # config's "[%]" unit literally: each event adds that percentage of
+            # the initial modifier -- the reading the paper's env2 HF-DBS row
+            # agrees with (statistical anchors).
+            mode = p.get("encapsulation_mode", "raw")
+            if mode == "relative":
+                self.encaps_precent = p["encapsulation_percent"] * 0.01 * p["conduct_modifier"]
+            elif mode != "raw":
+                raise ValueError(f"encapsulation_mode {mode!r}: expected 'raw' or 'relative'")
             # env.py:368 asserts plasticity_drift_freq >= 2, which makes every shipped
             # env2 config unconstructible; the paper-era code had no such assert
             # (SURVEY.md Appendix C1), so it is not enforced here.

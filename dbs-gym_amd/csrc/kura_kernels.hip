@@ -473,6 +473,11 @@ __device__ __forceinline__ void store8(const Slot& w, int slot, int t, const flo
     // (one column tile per wave) they intermittently lost record components
     // on gfx950 (ROCm 7.2), see DESIGN.md "Kernel notes".
     const floatx4 a = {v[0], v[1], v[2], v[3]}, b = {v[4], v[5], v[6], v[7]};
+#ifdef KURA_BUFSTORE  // diagnostic build: the raw buffer store form (tools/parity_probe.py)
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u32, a), w.rs, w.voff, w.soff(slot, t), 0);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u32, b), w.rs, w.voff + 1024, w.soff(slot, t), 0);
+    return;
+#endif
     __attribute__((address_space(1))) char* sb = (__attribute__((address_space(1))) char*)w.base + w.soff(slot, t);
     *(gfx4*)(sb + (uint32_t)w.voff) = a;
     *(gfx4*)(sb + (uint32_t)(w.voff + 1024)) = b;

@@ -1,0 +1,44 @@
+"""The reference's evaluation protocol (aDBS_RL/evaluate_HF_DBS.py) run
+through the CPU oracle -- TEST INFRASTRUCTURE for tests/test_paper_anchors.py
+and tests/golden/make_anchor_oracle.py.  The draws come from the product's
+``evaluation.protocol_draws`` (pinned to the reference by
+tests/golden/make_golden_resets.py); the dynamics from oracle/kura_oracle.c,
+the metric from the restatement oracle/kura_eval.py."""
+from __future__ import annotations
+
+import importlib
+
+import numpy as np
+
+from helpers import ko, kura
+
+ev = importlib.import_module("dbs-gym_amd.evaluation")
+sim = importlib.import_module("dbs-gym_amd.sim")
+
+
+def oracle_protocol(name, n_episodes, actions=(0.0, 1.0), n_envs=5, psd_dt=5e-4, beta=(12.5, 21.0), **overrides):
+    """Returns bbpow [n_actions, n_envs] and the concatenated theta_mean signals."""
+    from oracle import kura_eval
+    plist, draws = ev.protocol_draws(name, n_episodes, n_envs, **overrides)
+    B = len(actions) * n_envs
+    cfg = sim.make_config(plist[0], B, reward_func="bbpow_action")
+    _, shared = kura.build_batch([p for _ in actions for p in plist])
+    o = ko.Oracle(cfg, shared["alpha"].astype(np.float32))
+    o.set_gain(shared["gain"])
+    bins = kura.spectral.beta_bins(cfg.window, plist[0]["verbose_dt"])
+    o.set_spectral(*kura.spectral.twiddles(cfg.window, bins))
+    a = np.array([[x] for x in actions for _ in range(n_envs)], np.float32)
+    sig = [[] for _ in range(B)]
+    for e in range(n_episodes):   # every env ends its episode on the same step: reset all together
+        d = [draws[k][1 + e] for _ in actions for k in range(n_envs)]
+        o.set_env_params(np.stack([x[0] for x in d]).astype(np.float32), np.stack([x[1] for x in d]),
+                         np.stack([x[2] for x in d]))
+        o.reset(np.stack([x[3] for x in d]).astype(np.float32))
+        for _ in range(cfg.episode_steps):
+            out = o.step(a)
+            for b in range(B):
+                sig[b].append(out["lfp_true"][b, :out["nsamp"][b]])
+    o.close()
+    sig = [np.concatenate(x) for x in sig]
+    bb = kura_eval.calc_psd_for_simple_eval(sig, psd_dt, beta[0], beta[1])
+    return bb.reshape(len(actions), n_envs), sig

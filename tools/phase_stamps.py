@@ -40,23 +40,32 @@ def main():
     sim.set_env_gain(gain)
     sim.set_env_params(omega, gs, gr)
     sim.set_spectral(ct, st)
-    sim.reset(torch.from_numpy(th0))
-    torch.cuda.synchronize()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     sim.stamps()
+    ev0.record()
+    sim.reset(torch.from_numpy(th0))
+    ev1.record()
+    torch.cuda.synchronize()
+    s_reset = sim.stamps().astype(np.float64)
+    ms_reset = ev0.elapsed_time(ev1)
     a = torch.zeros((cfg.n_envs, cfg.n_elec), device="cuda")
     nsteps = 5
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     ev0.record()
     for _ in range(nsteps):
         sim.step(a)
     ev1.record()
     torch.cuda.synchronize()
     s = sim.stamps().astype(np.float64)
+    if os.environ.get("MODE") == "reset":  # the reset transient's breakdown instead (one launch)
+        s, nsteps = s_reset, 1
+        ev_ms = ms_reset
+    else:
+        ev_ms = ev0.elapsed_time(ev1) / nsteps
     tot = s.sum(axis=1, keepdims=True)
     share = (s / np.maximum(tot, 1)).mean(axis=0)
     nwg = (cfg.n_envs + 15) // 16
     cyc_per_step_wave = s.sum(axis=0) / (8 * nwg * nsteps)
-    out = {"ms_per_step": ev0.elapsed_time(ev1) / nsteps,
+    out = {"mode": os.environ.get("MODE", "step"), "ms_per_launch": ev_ms,
            "share": dict(zip(PHASES, [round(float(x), 4) for x in share])),
            "cycles_per_step_per_wave": dict(zip(PHASES, [round(float(x)) for x in cyc_per_step_wave])),
            # per wave (rows), cycles per step of the phases that differ between waves
