@@ -16,6 +16,18 @@ KURA_S_MAX = 32
 KURA_MAX_BINS = 32
 KURA_NSTATS = 8
 
+# per-env failure bits (kura.h KURA_F_*)
+KURA_F_MAX_STEPS = 1
+KURA_F_NONFINITE = 2
+KURA_F_GRID = 8
+KURA_F_BARRIER = 16
+FLAG_NAMES = {
+    KURA_F_MAX_STEPS: "The maximum number of solver steps was reached",   # diffrax's message (throw=True)
+    KURA_F_NONFINITE: "non-finite (NaN/Inf) state or RHS",
+    KURA_F_GRID: "save grid outside [2, KURA_S_MAX] samples",
+    KURA_F_BARRIER: "split-group barrier timed out",
+}
+
 KURA_REC_NAIVE = 0
 KURA_REC_GAUSSIAN = 1
 KURA_R_BBPOW = 1
@@ -99,6 +111,7 @@ _SYMBOLS = {
     "kura_envelope_stats": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int, c_void_p, c_void_p]),
     "kura_episode_envelope_stats": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p]),
     "kura_get_stats": (c_int, [c_void_p, c_void_p, c_int]),
+    "kura_get_env_flags": (c_int, [c_void_p, c_void_p, c_void_p]),
     "kura_get_stamps": (c_int, [c_void_p, c_void_p]),
     "kura_selftest_math": (c_int, [c_void_p, c_void_p, c_void_p, c_int]),
     "kura_selftest_gemm": (c_int, [c_void_p, c_void_p, c_void_p, c_int]),
@@ -132,6 +145,22 @@ def load_library(path: str | None = None) -> ctypes.CDLL:
     return lib
 
 
+class KuraSolverError(RuntimeError):
+    """A solve failed inside kura_step/kura_reset (the reference's diffeqsolve
+    raises in these cases, diffrax throw=True, env.py:261-270).  ``envs``:
+    failing env indices, ``flags``: their KURA_F_* bits."""
+
+    def __init__(self, what, envs, flags):
+        self.envs, self.flags = list(envs), list(flags)
+        kinds = sorted({name for f in self.flags for bit, name in FLAG_NAMES.items() if f & bit})
+        shown = ", ".join(f"{e}:{f}" for e, f in list(zip(self.envs, self.flags))[:8])
+        super().__init__(f"{what}: {'; '.join(kinds)} (env:flags {shown}{' ...' if len(self.envs) > 8 else ''})")
+
+
+def describe_flags(f: int) -> str:
+    return "; ".join(name for bit, name in FLAG_NAMES.items() if f & bit) or "ok"
+
+
 def check(lib: ctypes.CDLL, rc: int, what: str) -> None:
     if rc != 0:
         msg = lib.kura_last_error()
@@ -149,7 +178,8 @@ def ptr(a) -> int | None:
 
 
 __all__ = [
-    "KuraConfig", "load_library", "check", "ptr", "LIB_PATH",
+    "KuraConfig", "load_library", "check", "ptr", "LIB_PATH", "KuraSolverError", "describe_flags",
+    "KURA_F_MAX_STEPS", "KURA_F_NONFINITE", "KURA_F_GRID", "KURA_F_BARRIER",
     "KURA_ABI_VERSION", "KURA_S_MAX", "KURA_MAX_BINS", "REWARD_KINDS", "REC_KERNELS",
     "KURA_REC_NAIVE", "KURA_REC_GAUSSIAN", "KURA_R_BBPOW", "KURA_R_TEMP_CONST", "KURA_R_BBPOW_THR",
     "c_int64", "c_uint8",

@@ -105,6 +105,7 @@ struct DevParams {
     float* ep_lfp;          // [B][episode_cap] theta_mean samples of the running episode
     int* ep_len;            // [B] samples appended since the env's last reset
     int desync_cycles;      // odd workgroups start this many cycles late (spreads record bursts)
+    int* eflags;            // [B] per-env failure bits of the last launch (KURA_F_*, kura.h), 0 = ok
 };
 
 // Diagnostic phase timers (compile with -DKURA_STAMPS): per wave, cycles
@@ -681,8 +682,8 @@ __device__ __noinline__ void group_barrier(const DevParams& p, Part& pt) {
             if (++spins > XL_SPIN_MAX ||
                 (__hip_atomic_load((__attribute__((address_space(1))) unsigned long long*)&p.stats[3],
                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) &
-                 16ull)) {
-                atomicOr(&p.stats[3], 16ull);
+                 (unsigned long long)KURA_F_BARRIER)) {
+                atomicOr(&p.stats[3], (unsigned long long)KURA_F_BARRIER);
                 break;
             }
         }
@@ -953,8 +954,14 @@ __device__ __forceinline__ void post_step(const DevParams& p, const Slot& ws, in
         CtlE& c = s_ctl[tid];
         c.nsave = 0;
         c.keep = 0;
+        const float mean = etot[0] / (float)NG;
+        if (c.active && !(mean <= 3.40282346638528859812e+38f)) {
+            // non-finite state or RHS (NaN/Inf reaches the error norm): the
+            // solve fails here, as in the oracle (KURA_F_NONFINITE)
+            c.flags |= KURA_F_NONFINITE;
+            c.active = 0;
+        }
         if (c.active) {
-            const float mean = etot[0] / (float)NG;
             const float err = sqrtf(mean);
             const bool keep = err < 1.0f;
             float fac = 0.9f * kdm_inv_fifth_root(err);
@@ -1026,7 +1033,7 @@ __device__ __forceinline__ void post_step(const DevParams& p, const Slot& ws, in
             c.nsteps++;
             if (!(c.tprev < c.t1)) c.active = 0;
             if (c.active && c.nsteps >= p.max_steps) {
-                c.flags |= 1;
+                c.flags |= KURA_F_MAX_STEPS;
                 c.active = 0;
             }
         }
@@ -1430,6 +1437,15 @@ __device__ void r2_filters_wg(const DevParams& p, int env_base, double (&out)[EN
     }
 }
 
+// Launch-wide failure bits an env inherits: a split-group barrier that timed
+// out (group_barrier) leaves every later exchange of the launch unsynchronised.
+__device__ __forceinline__ int launch_flags(const DevParams& p, bool xl) {
+    if (!xl) return 0;
+    const unsigned long long v = __hip_atomic_load((__attribute__((address_space(1))) unsigned long long*)&p.stats[3],
+                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return (int)(v & KURA_F_BARRIER);
+}
+
 template <int TPW, bool XL>
 __device__ __forceinline__ void step_pair(const DevParams& p, Part& pt, float* Xs, const float* __restrict__ action,
                                           float* __restrict__ obs, double* __restrict__ reward,
@@ -1464,7 +1480,7 @@ __device__ __forceinline__ void step_pair(const DevParams& p, Part& pt, float* X
             ctl_begin(s_ctl[tid], g, p.dt0, 0, g.n, 0);
             if (g.n < 2 || g.n > KURA_S_MAX) {
                 s_ctl[tid].active = 0;
-                s_ctl[tid].flags |= 8;
+                s_ctl[tid].flags |= KURA_F_GRID;
             }
         }
     }
@@ -1499,7 +1515,7 @@ __device__ __forceinline__ void step_pair(const DevParams& p, Part& pt, float* X
             ctl_begin(c, g, p.dt0, 1, g.n - 1, nI + 1);
             if (g.n < 2 || nI + g.n - 1 > KURA_S_MAX) {
                 c.active = 0;
-                c.flags |= 8;
+                c.flags |= KURA_F_GRID;
             } else {  // ys_II[0] == ys_I[-1]: duplicated sample (env.py:440)
                 s_smp_n[tid][nI] = s_smp_n[tid][nI - 1];
                 s_smp_r[tid][nI] = s_smp_r[tid][nI - 1];
@@ -1525,7 +1541,11 @@ __device__ __forceinline__ void step_pair(const DevParams& p, Part& pt, float* X
         if (env >= p.B) continue;
         const CtlE& c = s_ctl[e];
         const int S = s_nI[e] + s_nII[e] - 1;
-        if (c.flags || S < 1) {
+        const int fl = c.flags | launch_flags(p, XL);
+        if (lane == 0) p.eflags[env] = fl;
+        if (fl || S < 1) {
+            // failed step (kura.h KURA_F_*): no state advance, done = 1; the
+            // host raises (diffrax's throw=True) or resets the env
             if (lane == 0) {
                 if (nsamp) nsamp[env] = 0;
                 if (done) done[env] = 1;
@@ -1633,6 +1653,7 @@ __device__ __forceinline__ void reset_pair(const DevParams& p, Part& pt, float* 
         const int env = env_base + e;
         if (env >= p.B || (mask && !mask[env])) continue;
         if (lane == 0) {
+            p.eflags[env] = s_ctl[e].flags | launch_flags(p, XL);
             p.t[env] = grid_at_c(s_ctl[e], s_ctl[e].n - 1);
             p.step[env] = 0;
             p.wpos[env] = 0;

@@ -15,7 +15,7 @@ import torch
 
 from . import abi
 from . import spectral
-from .abi import KURA_S_MAX, KuraConfig, check, ptr
+from .abi import KURA_S_MAX, KuraConfig, KuraSolverError, check, ptr
 
 
 def make_config(params: dict, n_envs: int, reward_func: str | None = None, max_steps: int = 4096,
@@ -96,6 +96,7 @@ class KuraSim:
         self.lfp_true = torch.zeros((B, KURA_S_MAX), dtype=torch.float32, device=dev)
         self.lfp_rec = torch.zeros((B, KURA_S_MAX), dtype=torch.float64, device=dev)
         self.nsamp = torch.zeros(B, dtype=torch.int32, device=dev)
+        self.flags = torch.zeros(B, dtype=torch.int32, device=dev)   # KURA_F_* of the last launch
 
     # ---- setup --------------------------------------------------------------
     def set_coupling(self, alpha: np.ndarray) -> None:
@@ -127,7 +128,9 @@ class KuraSim:
     def _stream(self):
         return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
 
-    def reset(self, theta0: torch.Tensor, mask: torch.Tensor | None = None) -> torch.Tensor:
+    def reset(self, theta0: torch.Tensor, mask: torch.Tensor | None = None, check_errors: bool = False):
+        """check_errors: synchronise and raise KuraSolverError if a masked
+        env's transient failed (otherwise see ``flags`` / ``raise_on_failure``)."""
         th = theta0.to(self.device, torch.float32).contiguous()
         if th.shape != (self.B, self.N):
             raise ValueError("theta0 must be (B, N)")
@@ -135,10 +138,18 @@ class KuraSim:
         with torch.cuda.device(self.device):
             check(self.lib, self.lib.kura_reset(self._h, ptr(m), ptr(th), ptr(self.obs), self._stream()),
                   "kura_reset")
+            check(self.lib, self.lib.kura_get_env_flags(self._h, ptr(self.flags), self._stream()),
+                  "kura_get_env_flags")
         self._keep = (th, m)  # keep inputs alive until the stream consumes them
+        if check_errors:
+            self.raise_on_failure("kura_reset", m)
         return self.obs
 
-    def step(self, action: torch.Tensor):
+    def step(self, action: torch.Tensor, check_errors: bool = False):
+        """One reference step() for every env.  Failed solves never throw in
+        the library (kura.h KURA_F_*): the env reports done = 1 and its bits
+        land in ``flags``; check_errors=True synchronises and raises
+        KuraSolverError as the reference's diffeqsolve would."""
         a = action.to(self.device, torch.float32).contiguous()
         if a.numel() != self.B * self.cfg.n_elec:
             raise ValueError("action must have B * n_elec elements")
@@ -146,8 +157,25 @@ class KuraSim:
             check(self.lib, self.lib.kura_step(self._h, ptr(a), ptr(self.obs), ptr(self.reward), ptr(self.done),
                                                ptr(self.lfp_true), ptr(self.lfp_rec), ptr(self.nsamp),
                                                self._stream()), "kura_step")
+            check(self.lib, self.lib.kura_get_env_flags(self._h, ptr(self.flags), self._stream()),
+                  "kura_get_env_flags")
         self._keep = (a,)
+        if check_errors:
+            self.raise_on_failure("kura_step")
         return self.obs, self.reward, self.done
+
+    def failed_envs(self, mask: torch.Tensor | None = None):
+        """(env indices, KURA_F_* bits) of the envs whose last launch failed (synchronises)."""
+        f = self.flags.cpu().numpy()
+        if mask is not None:
+            f = np.where(mask.cpu().numpy().astype(bool), f, 0)
+        idx = np.nonzero(f)[0]
+        return idx, f[idx]
+
+    def raise_on_failure(self, what: str = "kura_step", mask: torch.Tensor | None = None) -> None:
+        idx, fl = self.failed_envs(mask)
+        if len(idx):
+            raise KuraSolverError(what, idx.tolist(), fl.tolist())
 
     def reward_of(self, window: torch.Tensor, u0: torch.Tensor, kind: int = 0) -> torch.Tensor:
         w = window.to(self.device, torch.float64).contiguous()

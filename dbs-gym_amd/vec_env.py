@@ -21,6 +21,7 @@ import torch
 from . import spectral
 from .abi import KURA_S_MAX
 from .batch import EnvHost, build_batch, fill_driver_arrays
+from .abi import KuraSolverError
 from .sim import KuraSim, make_config
 
 
@@ -52,13 +53,24 @@ class KuraVectorEnv:
     autoreset:  SB3 DummyVecEnv semantics -- a finished env is reset inside the
                 same step() and its last observation is returned in
                 ``infos["terminal_observation"]``.
+    on_failure: a solve that fails inside the library (kura.h KURA_F_*:
+                max_steps, non-finite state, ...) -- "raise" (default) raises
+                KuraSolverError from step()/reset(), as the reference's
+                diffeqsolve does (diffrax throw=True, env.py:261-270);
+                "reset" reports the env terminated + truncated with
+                ``infos["failed_env_ids"]``/``infos["failure_flags"]`` and
+                autoresets it.
     """
 
     metadata = {"render.modes": ["human"]}
 
     def __init__(self, params, num_envs: int | None = None, device=0, reward_func: str | None = None,
                  w0_seed: int = 228, rand_seeds=None, autoreset: bool = True, max_steps: int = 4096,
-                 episode_metrics: bool = False, psd_dt: float = 5e-4, beta_band=(12.5, 21.0)):
+                 episode_metrics: bool = False, psd_dt: float = 5e-4, beta_band=(12.5, 21.0),
+                 on_failure: str = "raise"):
+        if on_failure not in ("raise", "reset"):
+            raise ValueError(f"on_failure={on_failure!r}: expected 'raise' or 'reset'")
+        self.on_failure = on_failure
         if isinstance(params, dict):
             if num_envs is None:
                 raise ValueError("num_envs is required with a single params dict")
@@ -105,6 +117,9 @@ class KuraVectorEnv:
 
     # ---- gymnasium VectorEnv API --------------------------------------------
     def _draw(self, idx):
+        """Host draws of reset() for the envs in idx; uploads only their
+        parameters (one kura_set_env_params per contiguous run of envs)."""
+        idx = sorted(int(b) for b in idx)
         th = np.zeros((self.num_envs, self.N), np.float32)
         for b in idx:
             w0, gs, gr, th0 = self.hosts[b].reset_draws()
@@ -112,7 +127,14 @@ class KuraVectorEnv:
             self._g_stim[b] = gs
             self._g_rec[b] = gr
             th[b] = th0.astype(np.float32)
-        self.sim.set_env_params(self._omega, self._g_stim, self._g_rec)
+        k = 0
+        while k < len(idx):
+            j = k
+            while j + 1 < len(idx) and idx[j + 1] == idx[j] + 1:
+                j += 1
+            a, b = idx[k], idx[j] + 1
+            self.sim.set_env_params(self._omega[a:b], self._g_stim[a:b], self._g_rec[a:b], env0=a)
+            k = j + 1
         return torch.from_numpy(th).to(self.device)
 
     def reset(self, seed=None, options=None):
@@ -124,6 +146,7 @@ class KuraVectorEnv:
                 h.rs.seed(int(s))
         th = self._draw(range(self.num_envs))
         obs = self.sim.reset(th)
+        self._check_reset(None)
         self.steps[:] = 0
         self._was_reset = True
         return obs.view(self.num_envs, 1, self.W).clone(), {}
@@ -142,6 +165,16 @@ class KuraVectorEnv:
         infos: dict = {}
         term_host = self.steps >= self.episode_steps
         terminated = done.bool().clone()
+        truncated = torch.zeros_like(terminated)
+        failed, fflags = self.sim.failed_envs()          # synchronises: the step's outputs are ready
+        if len(failed):
+            if self.on_failure == "raise":
+                raise KuraSolverError("kura_step", failed.tolist(), fflags.tolist())
+            infos["failed_env_ids"] = failed
+            infos["failure_flags"] = fflags
+            truncated[torch.as_tensor(failed, device=self.device)] = True
+            term_host = term_host.copy()
+            term_host[failed] = True                     # autoreset keys on the same envs the flags name
         if term_host.any():
             idx = np.nonzero(term_host)[0]
             infos["terminal_env_ids"] = idx
@@ -160,9 +193,13 @@ class KuraVectorEnv:
             mask[idx] = 1
             th = self._draw(idx)
             self.sim.reset(th, mask.to(self.device))
+            self._check_reset(mask)
             self.steps[idx] = 0
-        truncated = torch.zeros_like(terminated)
         return obs.view(self.num_envs, 1, self.W).clone(), rew.clone(), terminated, truncated, infos
+
+    def _check_reset(self, mask):
+        if self.on_failure == "raise":
+            self.sim.raise_on_failure("kura_reset", None if mask is None else mask.to(self.device))
 
     # ---- attributes read by the reference's callers ----------------------------
     @property

@@ -47,6 +47,19 @@ enum {
     KURA_E_STATE = -5      /* call order violated (e.g. step before reset) */
 };
 
+/* per-env failure bits of a step/reset launch (kura_get_env_flags, and OR-ed
+ * over the launch into kura_get_stats()[3]).  The reference's diffeqsolve
+ * raises on a failed solve (diffrax throw=True, env.py:261-270); libkura never
+ * throws: a failed env's step is abandoned (state not advanced, done = 1,
+ * reward = 0, nsamp = 0, obs/lfp not written) and the host decides. */
+enum {
+    KURA_F_MAX_STEPS = 1,   /* diffeqsolve max_steps reached */
+    KURA_F_NONFINITE = 2,   /* NaN/Inf state or RHS (non-finite error norm) */
+    KURA_F_GRID = 8,        /* save grid outside [2, KURA_S_MAX] samples */
+    KURA_F_BARRIER = 16     /* split-group (N > 1024) barrier timed out: every
+                               exchange after it is unsynchronised */
+};
+
 enum { KURA_REC_NAIVE = 0, KURA_REC_GAUSSIAN = 1 };             /* env.py:333-338 */
 enum { KURA_R_BBPOW = 1, KURA_R_TEMP_CONST = 2, KURA_R_BBPOW_THR = 3 }; /* env.py:323-330 */
 
@@ -158,10 +171,15 @@ int kura_get_state(KuraHandle* h, float* y /* B*N */, double* t /* B */, int32_t
                    double* ring /* B*W */, int32_t* wpos /* B */);
 int kura_set_state(KuraHandle* h, const float* y, const double* t, const int32_t* step,
                    const double* ring, const int32_t* wpos);
+/* per-env KURA_F_* bits of the last kura_step / kura_reset (0 = ok), copied
+ * into the caller's device buffer out_dev (B int32) on the given stream:
+ * read them with the step's outputs (no extra synchronisation). */
+int kura_get_env_flags(KuraHandle* h, int32_t* out_dev, void* stream);
+
 /* counters (synchronises the device), first min(n, KURA_NSTATS) written:
  * last call:  [0] RHS sweeps issued by the busiest workgroup, [1] Dopri5 steps
- *             attempted (all envs), [2] rejected, [3] error flags (bit0
- *             max_steps, bit3 grid overflow), [4] RHS sweeps issued summed over
+ *             attempted (all envs), [2] rejected, [3] KURA_F_* bits OR-ed over
+ *             the envs, [4] RHS sweeps issued summed over
  *             workgroups (each sweep covers 16 env slots);
  * since kura_create: [5] steps attempted, [6] workgroup sweeps, [7] rejected. */
 #define KURA_NSTATS 8

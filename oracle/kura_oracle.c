@@ -375,7 +375,7 @@ static void solve(const OCtx* o, Work* w, const Grid* g, float* y_start, const f
     int64_t nsteps = 0;
     float* const* F = w->F;
     while (tprev < t1) {
-        if (nsteps >= cfg->max_steps) { st->flags |= 1; break; }
+        if (nsteps >= cfg->max_steps) { st->flags |= KURA_F_MAX_STEPS; break; }
         ++nsteps;
         const float h = tnext - tprev;
         /* stages 2..7: ys = y0 + chain(a_ij * k_j), k_j = h*F[j] */
@@ -422,6 +422,9 @@ static void solve(const OCtx* o, Work* w, const Grid* g, float* y_start, const f
             w->cosrow[i] = q * q; /* scratch */
         }
         float mean = oracle_rm_f32(w->cosrow, N) / (float)N;
+        /* non-finite state or RHS reaches the error norm: the solve fails
+         * (KURA_F_NONFINITE; the kernel's post_step makes the same test) */
+        if (!(mean <= 3.40282346638528859812e+38f)) { st->flags |= KURA_F_NONFINITE; break; }
         float err = sqrtf(mean);
         int keep = err < 1.0f;
         float fac = 0.9f * kdm_inv_fifth_root(err);
@@ -478,8 +481,6 @@ static void solve(const OCtx* o, Work* w, const Grid* g, float* y_start, const f
         tnext = tn;
     }
     if (!(tprev < t1) && si < n) st->flags |= 4; /* unreachable: grid not fully saved */
-    for (int i = 0; i < N; ++i)
-        if (y_start[i] != y_start[i]) { st->flags |= 2; break; }
 }
 
 /* ----------------------------------------------------------------- rewards */
@@ -560,7 +561,8 @@ static double rescale_action(const KuraConfig* c, float a) {
 /* reset(): transient solve from theta0 over arange(0, transient_len, dt);
  * window = last W of LFP(rows[:-1]).  Arrays are B-major. */
 int oracle_reset(void* ctx, int B, const float* omega, const double* g_rec, const float* theta0, float* y,
-                 double* t, int32_t* step, double* ring, int32_t* wpos, float* obs, int64_t* stats_out) {
+                 double* t, int32_t* step, double* ring, int32_t* wpos, float* obs, int64_t* stats_out,
+                 int32_t* eflags) {
     OCtx* o = (OCtx*)ctx;
     const KuraConfig* cfg = &o->cfg;
     const int N = o->N, W = cfg->window;
@@ -586,6 +588,7 @@ int oracle_reset(void* ctx, int B, const float* omega, const double* g_rec, cons
             step[b] = 0;
             for (int i = 0; i < W; ++i) ring[(size_t)b * W + i] = lr[i];
             wpos[b] = 0;
+            if (eflags) eflags[b] = (int32_t)st.flags;
             if (obs)
                 for (int i = 0; i < W; ++i) obs[(size_t)b * W + i] = (float)lr[i];
 #pragma omp critical
@@ -609,7 +612,7 @@ int oracle_reset(void* ctx, int B, const float* omega, const double* g_rec, cons
 int oracle_step(void* ctx, int B, const float* omega, const double* g_stim, const double* g_rec,
                 const double* ctab, const double* stab, const float* action, float* y, double* t,
                 int32_t* step, double* ring, int32_t* wpos, float* obs, double* reward, uint8_t* done,
-                float* lfp_true, double* lfp_rec, int32_t* nsamp, int64_t* stats_out) {
+                float* lfp_true, double* lfp_rec, int32_t* nsamp, int64_t* stats_out, int32_t* eflags) {
     OCtx* o = (OCtx*)ctx;
     const KuraConfig* cfg = &o->cfg;
     const int N = o->N, W = cfg->window, NE = cfg->n_elec;
@@ -642,20 +645,22 @@ int oracle_step(void* ctx, int B, const float* omega, const double* g_stim, cons
             Grid gI = arange(t[b], t[b] + cfg->width, cfg->dt);
             Grid gII;
             int nI = gI.n;
-            if (nI < 2 || nI > KURA_S_MAX) { st.flags |= 8; goto done_env; }
+            if (nI < 2 || nI > KURA_S_MAX) { st.flags |= KURA_F_GRID; goto fail_env; }
             {
                 Sink sI = {NULL, lfN, lfR, 0, nI, grb};
                 solve(o, &w, &gI, yb, wb, pulse, &sI, &st);
+                if (st.flags) goto fail_env;   /* no OFF solve: the step is abandoned */
                 double tm = grid_at(&gI, nI - 1);
                 /* II: stimulation OFF */
                 gII = arange(tm, tm + cfg->pause, cfg->dt);
                 int nII = gII.n;
                 int S = nI + nII - 1;
-                if (nII < 2 || S > KURA_S_MAX) { st.flags |= 8; goto done_env; }
+                if (nII < 2 || S > KURA_S_MAX) { st.flags |= KURA_F_GRID; goto fail_env; }
                 lfN[nI] = lfN[nI - 1]; /* ys_II[0] == ys_I[-1] (duplicate row, env.py:440) */
                 lfR[nI] = lfR[nI - 1];
                 Sink sII = {NULL, lfN + nI + 1, lfR + nI + 1, 1, nII - 1, grb};
                 solve(o, &w, &gII, yb, wb, w.zero, &sII, &st);
+                if (st.flags) goto fail_env;
                 t[b] = grid_at(&gII, nII - 1);
                 /* window: append S records, keep last W (env.py:447-448) */
                 double* rb = ring + (size_t)b * W;
@@ -679,7 +684,14 @@ int oracle_step(void* ctx, int B, const float* omega, const double* g_stim, cons
                     if (lfp_rec) lfp_rec[(size_t)b * KURA_S_MAX + s] = s < S ? lfR[s] : 0.0;
                 }
                 nsamp[b] = S;
+                if (eflags) eflags[b] = 0;
+                goto done_env;
             }
+        fail_env: /* kura.h KURA_F_*: t/step/window not advanced, done = 1 */
+            done[b] = 1;
+            reward[b] = 0.0;
+            nsamp[b] = 0;
+            if (eflags) eflags[b] = (int32_t)st.flags;
         done_env:
 #pragma omp critical
             {

@@ -35,9 +35,9 @@ def lib() -> ctypes.CDLL:
         L.oracle_create.argtypes = [c_void_p, c_void_p]
         L.oracle_destroy.argtypes = [c_void_p]
         L.oracle_reset.restype = c_int
-        L.oracle_reset.argtypes = [c_void_p, c_int] + [c_void_p] * 10
+        L.oracle_reset.argtypes = [c_void_p, c_int] + [c_void_p] * 11
         L.oracle_step.restype = c_int
-        L.oracle_step.argtypes = [c_void_p, c_int] + [c_void_p] * 18
+        L.oracle_step.argtypes = [c_void_p, c_int] + [c_void_p] * 19
         L.oracle_solve_rows.restype = c_int
         L.oracle_solve_rows.argtypes = [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p]
         L.oracle_rhs.argtypes = [c_void_p] * 5
@@ -80,6 +80,7 @@ class Oracle:
         self.ring = np.zeros((B, W), np.float64)
         self.wpos = np.zeros(B, np.int32)
         self.stats = np.zeros(4, np.int64)
+        self.flags = np.zeros(B, np.int32)   # KURA_F_* of the last reset/step per env
 
     def set_env_params(self, omega, g_stim, g_rec=None):
         self.omega = np.ascontiguousarray(omega, np.float32)
@@ -100,7 +101,8 @@ class Oracle:
         th = np.ascontiguousarray(theta0, np.float32)
         obs = np.zeros((self.B, self.W), np.float32)
         rc = lib().oracle_reset(self._ctx, self.B, _p(self.omega), _p(self.g_rec), _p(th), _p(self.y), _p(self.t),
-                                _p(self.step_count), _p(self.ring), _p(self.wpos), _p(obs), _p(self.stats))
+                                _p(self.step_count), _p(self.ring), _p(self.wpos), _p(obs), _p(self.stats),
+                                _p(self.flags))
         assert rc == 0
         return obs
 
@@ -113,7 +115,8 @@ class Oracle:
         rc = lib().oracle_step(self._ctx, B, _p(self.omega), _p(self.g_stim), _p(self.g_rec), _p(self.ctab),
                                _p(self.stab), _p(a), _p(self.y), _p(self.t), _p(self.step_count), _p(self.ring),
                                _p(self.wpos), _p(out["obs"]), _p(out["reward"]), _p(out["done"]),
-                               _p(out["lfp_true"]), _p(out["lfp_rec"]), _p(out["nsamp"]), _p(self.stats))
+                               _p(out["lfp_true"]), _p(out["lfp_rec"]), _p(out["nsamp"]), _p(self.stats),
+                               _p(self.flags))
         assert rc == 0
         return out
 

