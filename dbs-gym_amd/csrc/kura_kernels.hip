@@ -106,6 +106,7 @@ struct DevParams {
     int* ep_len;            // [B] samples appended since the env's last reset
     int desync_cycles;      // odd workgroups start this many cycles late (spreads record bursts)
     int* eflags;            // [B] per-env failure bits of the last launch (KURA_F_*, kura.h), 0 = ok
+    float* rows;            // optional [B][KURA_S_MAX+1][N]: every saved row of a step (sol_state_, env.py:430,440)
 };
 
 // Diagnostic phase timers (compile with -DKURA_STAMPS): per wave, cycles
@@ -802,9 +803,20 @@ __device__ __forceinline__ void save_pass(const DevParams& p, const Slot& ws, in
     // identical in every wave: each wave holds all 16 envs
     const int anyw = __any(anyl) ? (anyl | __shfl_xor(anyl, 32, 64)) : 0;
     // rows that feed neither an LFP sample nor the final state (the first
-    // 3999 - W saves of the reset transient) need no evaluation at all
+    // 3999 - W saves of the reset transient) need no evaluation at all --
+    // unless the step's rows are captured (kura_set_row_capture)
     const int flor = fl[0] | fl[1] | fl[2] | fl[3] | fl[4] | fl[5] | fl[6] | fl[7];
-    const bool eval_rows = __any(flor & kEval);  // LFP or final-row bits of any round
+    constexpr int kSave = (int)(01111111111u & ((1u << (3 * RCX)) - 1u));
+    const bool capture = p.rows != nullptr && !to_ring;
+    const bool eval_rows = __any(flor & (capture ? kSave : kEval));  // rows to evaluate in any round
+    int rbase[8];  // captured row index of round 0 of this pass: sol_state_ row si - lfp_from + pos0
+    if (capture) {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const CtlE& c = s_ctl[mfma_env(q, lane)];
+            rbase[q] = c.si + r0 - c.lfp_from + c.pos0;
+        }
+    }
 #pragma unroll 1
     for (int t = 0; t < (eval_rows ? TPW : 0); ++t) {
         const int i = 32 * (wave * TPW + t) + (lane & 31);
@@ -843,6 +855,8 @@ __device__ __forceinline__ void save_pass(const DevParams& p, const Slot& ws, in
                 }
                 const int env = env_base + mfma_env(q, lane);
                 if ((f & 4) && env < p.B) p.y[(size_t)env * NG + col0 + i] = v;
+                if (capture && env < p.B)
+                    p.rows[((size_t)env * (KURA_S_MAX + 1) + rbase[q] + k) * NG + col0 + i] = v;
             }
         }
     }

@@ -1,0 +1,159 @@
+"""Stable-Baselines3-shaped VecEnv over a KuraVectorEnv.
+
+The reference's callers drive single ``SpatialKuramoto`` envs through SB3's
+``DummyVecEnv`` (+ ``Monitor``): ``train_aDBS_RL.py:116-193``,
+``aDBS_RL/evaluate_HF_DBS.py:33-119``, ``aDBS_RL/agents/custom_callbacks.py``.
+``KuraSB3VecEnv`` gives those call shapes to a GPU batch without importing
+stable-baselines3 (not installed here): it is duck-typed to SB3's ``VecEnv``
+
+* ``reset() -> obs`` (NumPy, ``(n_envs, 1, W)`` float32);
+* ``step(actions) -> (obs, rewards, dones, infos)`` with ``rewards`` float32
+  (DummyVecEnv's ``buf_rews``), ``dones`` bool, ``infos`` a list of per-env
+  dicts; a finished env is reset inside the same step and its last
+  observation is ``info["terminal_observation"]``; ``info["TimeLimit.truncated"]``
+  is set for ends that are not terminations;
+* ``step_async``/``step_wait``, ``get_attr``/``set_attr``/``env_method``,
+  ``env_is_wrapped``, ``seed``, ``close``;
+* ``monitor=True`` adds SB3 ``Monitor``'s episode summary
+  ``info["episode"] = {"r": round(sum of rewards, 6), "l": length, "t": seconds}``
+  and makes ``env_is_wrapped(Monitor)`` report True, which switches
+  ``evaluate_policy_`` (evaluate_HF_DBS.py:56,97-101) to the Monitor branch.
+"""
+from __future__ import annotations
+
+import time
+
+import numpy as np
+
+from .vec_env import KuraVectorEnv
+
+_REWARD_METHODS = ("reward_bbpow_action", "reward_temp_const_lfp_betafilt_action", "reward_bbpow_threth_action")
+
+
+class KuraSB3VecEnv:
+    def __init__(self, venv: KuraVectorEnv, monitor: bool = True):
+        if not venv.autoreset:
+            raise ValueError("KuraSB3VecEnv needs a KuraVectorEnv with autoreset=True (DummyVecEnv semantics)")
+        self.venv = venv
+        self.num_envs = venv.num_envs
+        self.observation_space = venv.single_observation_space
+        self.action_space = venv.single_action_space
+        self.render_mode = None
+        self.monitor = monitor
+        self._actions = None
+        self._ep_rew = np.zeros(self.num_envs, np.float64)
+        self._ep_len = np.zeros(self.num_envs, np.int64)
+        self._t0 = np.full(self.num_envs, time.time())
+
+    # ---- VecEnv core ----------------------------------------------------------
+    def reset(self):
+        obs, _ = self.venv.reset()
+        self._ep_rew[:] = 0.0
+        self._ep_len[:] = 0
+        self._t0[:] = time.time()
+        return obs.cpu().numpy()
+
+    def step_async(self, actions) -> None:
+        a = np.asarray(actions, dtype=np.float32).reshape(self.num_envs, -1)
+        self._actions = a
+
+    def step_wait(self):
+        if self._actions is None:
+            raise RuntimeError("step_wait() without step_async()")
+        a, self._actions = self._actions, None
+        obs, rew, term, trunc, info = self.venv.step(a)
+        rew64 = rew.cpu().numpy()
+        dones = (term | trunc).cpu().numpy().astype(bool)
+        trunc_h = trunc.cpu().numpy().astype(bool)
+        term_h = term.cpu().numpy().astype(bool)
+        obs_h = obs.cpu().numpy()
+        self._ep_rew += rew64
+        self._ep_len += 1
+        infos = [{} for _ in range(self.num_envs)]
+        ended = info.get("terminal_env_ids", np.zeros(0, np.int64))
+        if len(ended):
+            tobs = info["terminal_observation"].cpu().numpy()
+            now = time.time()
+            for j, b in enumerate(ended):
+                d = infos[b]
+                d["terminal_observation"] = tobs[j]
+                d["TimeLimit.truncated"] = bool(trunc_h[b] and not term_h[b])   # DummyVecEnv.step_wait
+                if self.monitor:
+                    d["episode"] = {"r": round(float(self._ep_rew[b]), 6), "l": int(self._ep_len[b]),
+                                    "t": round(now - self._t0[b], 6)}
+                for k in ("bbpow", "envelope"):
+                    if k in info.get("episode", {}):
+                        d.setdefault("episode_metrics", {})[k] = info["episode"][k][j]
+                self._ep_rew[b] = 0.0
+                self._ep_len[b] = 0
+                self._t0[b] = now
+        for k, key in (("failed_env_ids", "failure_flags"),):
+            if k in info:
+                for b, f in zip(info[k], info[key]):
+                    infos[b]["failure_flags"] = int(f)
+        return obs_h, rew64.astype(np.float32), dones, infos
+
+    def step(self, actions):
+        self.step_async(actions)
+        return self.step_wait()
+
+    def close(self) -> None:
+        self.venv.close()
+
+    def seed(self, seed=None):
+        """SB3 VecEnv.seed: env i gets seed + i at the next reset (np.random.seed per env)."""
+        if seed is None:
+            return [None] * self.num_envs
+        for i, h in enumerate(self.venv.hosts):
+            h.rs.seed(int(seed) + i)
+        return [int(seed) + i for i in range(self.num_envs)]
+
+    # ---- attribute / method access ------------------------------------------------
+    def _idx(self, indices):
+        if indices is None:
+            return list(range(self.num_envs))
+        if isinstance(indices, int):
+            return [indices]
+        return list(indices)
+
+    def get_attr(self, attr_name: str, indices=None):
+        return self.venv.get_attr(attr_name, self._idx(indices))
+
+    def set_attr(self, attr_name: str, value, indices=None) -> None:
+        for i in self._idx(indices):
+            if attr_name == "params_dict":
+                self.venv.params[i] = value
+            else:
+                raise AttributeError(f"set_attr({attr_name!r}) is not supported on the batched env")
+
+    def env_method(self, method_name: str, *args, indices=None, **kwargs):
+        """The reference env methods callers invoke through a VecEnv: the three
+        reward functions (env.py:638-688, aDBS_RL/agents/simple_dbs.py:83-90)."""
+        if method_name not in _REWARD_METHODS:
+            raise AttributeError(f"env_method({method_name!r}) is not supported on the batched env")
+        kind = 1 + _REWARD_METHODS.index(method_name)
+        x_state, action_value = args[0], args[1]
+        idx = self._idx(indices)
+        w = np.repeat(np.asarray(x_state, np.float64)[None, :], len(idx), axis=0)
+        u = np.full(len(idx), float(action_value[0]), np.float32)
+        return [float(v) for v in self.venv.reward_of(w, u, kind).cpu().numpy()]
+
+    def env_is_wrapped(self, wrapper_class, indices=None):
+        name = getattr(wrapper_class, "__name__", str(wrapper_class))
+        return [self.monitor and name == "Monitor"] * len(self._idx(indices))
+
+    def get_images(self):
+        return [None] * self.num_envs
+
+    def render(self, mode=None):
+        return None
+
+    @property
+    def unwrapped(self):
+        return self
+
+    def __len__(self):
+        return self.num_envs
+
+
+__all__ = ["KuraSB3VecEnv"]

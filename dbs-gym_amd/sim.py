@@ -164,6 +164,16 @@ class KuraSim:
             self.raise_on_failure("kura_step")
         return self.obs, self.reward, self.done
 
+    def capture_rows(self, on: bool = True) -> None:
+        """Keep every saved phase row of each step in ``self.rows`` (B, KURA_S_MAX+1, N):
+        rows 0..nsamp of env b are the reference's sol_state_ (env.py:430,440)."""
+        if on:
+            self.rows = torch.zeros((self.B, KURA_S_MAX + 1, self.N), dtype=torch.float32, device=self.device)
+            check(self.lib, self.lib.kura_set_row_capture(self._h, ptr(self.rows)), "kura_set_row_capture")
+        else:
+            check(self.lib, self.lib.kura_set_row_capture(self._h, None), "kura_set_row_capture")
+            self.rows = None
+
     def failed_envs(self, mask: torch.Tensor | None = None):
         """(env indices, KURA_F_* bits) of the envs whose last launch failed (synchronises)."""
         f = self.flags.cpu().numpy()

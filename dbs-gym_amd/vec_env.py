@@ -267,6 +267,7 @@ class SpatialKuramoto:
         self.params_dict = params_dict
         self._v = KuraVectorEnv([params_dict], device=device, rand_seeds=[params_dict["rand_seed"]],
                                 autoreset=False)
+        self._v.sim.capture_rows(True)          # sol_state_: every row of the step (env.py:430,440)
         self.action_space = self._v.single_action_space
         self.observation_space = self._v.single_observation_space
         self.current_step = 0
@@ -296,8 +297,9 @@ class SpatialKuramoto:
 
     @property
     def sol_state_(self):
-        """Last phase row (the reference keeps every saved row of the step)."""
-        return self._v.sim.get_state()["y"][:1]
+        """Every saved phase row of the last step, ys_I then ys_II (env.py:430,440): (nsamp + 1, N) float32."""
+        n = int(self._v.sim.nsamp[0].item())
+        return self._v.sim.rows[0, :n + 1].cpu().numpy()
 
     def _reward(self, kind, x_state, action_value):
         assert len(np.asarray(x_state).shape) == 1, "Incorrect dimension of theta_state"

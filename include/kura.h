@@ -171,6 +171,13 @@ int kura_get_state(KuraHandle* h, float* y /* B*N */, double* t /* B */, int32_t
                    double* ring /* B*W */, int32_t* wpos /* B */);
 int kura_set_state(KuraHandle* h, const float* y, const double* t, const int32_t* step,
                    const double* ring, const int32_t* wpos);
+/* optional capture of every saved phase row of each kura_step: rows_dev
+ * (device, B*(KURA_S_MAX+1)*N float32, or NULL to stop) receives, per env,
+ * rows 0 .. S of the step -- ys_I then ys_II, the reference's sol_state_
+ * (env.py:430,440; S = nsamp, row S is the new state).  Costs one extra
+ * store per saved value; off by default. */
+int kura_set_row_capture(KuraHandle* h, float* rows_dev);
+
 /* per-env KURA_F_* bits of the last kura_step / kura_reset (0 = ok), copied
  * into the caller's device buffer out_dev (B int32) on the given stream:
  * read them with the step's outputs (no extra synchronisation). */

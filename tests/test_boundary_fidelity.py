@@ -1,0 +1,50 @@
+"""Boundary details callers read: sol_state_ keeps every
+row of the step, get_attr('u') is the reference's rescale_action bit for bit."""
+import importlib
+
+import numpy as np
+import pytest
+
+from helpers import ko, kura
+
+
+def _reference_rescale(a, x=-1, y=1, z=-5, k=5):
+    """env.py:389-393 with float(a) (env.py:419): Python float arithmetic."""
+    return z + ((k - z) * (float(a) - x)) / (y - x)
+
+
+def test_u_formula_is_rescale_action():
+    torch = pytest.importorskip("torch")
+    rng = np.random.default_rng(0)
+    a = np.concatenate([rng.uniform(-1, 1, 20000), rng.uniform(-3, 3, 2000), [-1, 1, 0, -0.0, 0.5, 1e-8, -1e-30]]
+                       ).astype(np.float32)
+    # KuraVectorEnv.step: lo + ((hi - lo) * (a + 1.0)) / 2.0 in float64 -- the same IEEE operations
+    got = (-5.0 + ((5.0 - -5.0) * (torch.from_numpy(a).double() + 1.0)) / 2.0).numpy()
+    ref = np.array([_reference_rescale(v) for v in a])
+    np.testing.assert_array_equal(got, ref)
+
+
+@pytest.mark.gpu
+def test_single_env_sol_state_rows():
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    vec = importlib.import_module("dbs-gym_amd.vec_env")
+    p = kura.fill_driver_arrays(kura.reference_params("env1", "eval", 1), w0_seed=228)
+    p["reward_func"] = "bbpow_action"
+    env = vec.SpatialKuramoto(p)
+    o = ko.Oracle(env._v.cfg, kura.model_setup.coupling_alpha(p["neur_coords"]).astype(np.float32))
+    for k in range(5):
+        env.step([0.4 * (k - 2)])
+        rows = env.sol_state_
+        S = len(env.theta_mean)
+        assert rows.shape == (S + 1, env._v.N) and rows.dtype == np.float32
+        # row S is the new state, the I/II boundary row is duplicated (env.py:440)
+        np.testing.assert_array_equal(rows[S], env._v.sim.get_state()["y"][0])
+        # every LFP sample is the oracle's LFP of the captured row (RM-order reduction, bit for bit)
+        for s in range(S):
+            n, r = o.lfp(rows[s], env._v._g_rec[0])
+            assert n == env.theta_mean[s] and r == env.theta_records[s], (k, s)
+    # the duplicate row: ys_II[0] == ys_I[-1]; find it as two equal consecutive rows
+    assert any(np.array_equal(rows[i], rows[i + 1]) for i in range(2, 5))
+    env.close()
