@@ -490,7 +490,7 @@ __device__ __forceinline__ void store8(const Slot& w, int slot, int t, const flo
 // start of the solve; all TPW tiles' loads are issued before the first use)
 // (split groups read this part's sin/cos from its published global image)
 template <int TPW, bool XL>
-__device__ __forceinline__ void coupling_epilogue(const DevParams& p, const Slot& ws, const float* __restrict__ Xs,
+__device__ __forceinline__ void coupling_epilogue(const DevParams& __restrict__ p, const Slot& ws, const float* __restrict__ Xs,
                                                   const float* __restrict__ xown, const floatx16 (&acc)[TPW],
                                                   int stage, bool pulse_on, float (&fout)[TPW][8]) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -603,25 +603,65 @@ __device__ __forceinline__ void stage_input(const Slot& ws, float* Xs, int s, co
 // RM reduction (kura_detmath.h): per-lane partials (t order) -> 32-lane xor
 // butterfly -> s_red[k][wave][e]; the caller barriers, then thread e adds the
 // 8 wave totals in wave order.
+//
+// Only lanes 0 and 32 need the butterfly's result, so it is evaluated as the
+// same addition tree without shuffling through LDS: xor 16 crosses DPP rows
+// (ds_swizzle, bit-mask mode), then DPP row_shl:8/4/2/1 hand lane c+o's
+// partial to lane c -- at lane 0 this adds exactly the pairs the xor
+// butterfly adds there ((v0+v16) + (v8+v24)) + ..., a bit-exact twin of
+// oracle_rm_f32 (other lanes end with values nobody reads).
+__device__ __forceinline__ float dpp_shl(float v, int ctrl_sel) {
+    int x = __float_as_int(v);
+    switch (ctrl_sel) {  // row_shl:N = 0x100 + N (lane i reads lane i+N of its row of 16)
+        case 8: x = __builtin_amdgcn_mov_dpp(x, 0x108, 0xF, 0xF, false); break;
+        case 4: x = __builtin_amdgcn_mov_dpp(x, 0x104, 0xF, 0xF, false); break;
+        case 2: x = __builtin_amdgcn_mov_dpp(x, 0x102, 0xF, 0xF, false); break;
+        default: x = __builtin_amdgcn_mov_dpp(x, 0x101, 0xF, 0xF, false); break;
+    }
+    return __int_as_float(x);
+}
+__device__ __forceinline__ float rm_half_total(float v) {
+    v = v + __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(v), 0x401F));  // xor 16 (and 0x1F)
+    v = v + dpp_shl(v, 8);
+    v = v + dpp_shl(v, 4);
+    v = v + dpp_shl(v, 2);
+    v = v + dpp_shl(v, 1);
+    return v;
+}
+__device__ __forceinline__ double dpp_shl_d(double v, int n) {
+    const uint64_t u = __builtin_bit_cast(uint64_t, v);
+    const uint32_t lo = __float_as_uint(dpp_shl(__uint_as_float((uint32_t)u), n));
+    const uint32_t hi = __float_as_uint(dpp_shl(__uint_as_float((uint32_t)(u >> 32)), n));
+    return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+__device__ __forceinline__ double rm_half_total_d(double v) {
+    const uint64_t u = __builtin_bit_cast(uint64_t, v);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_swizzle((int)(uint32_t)u, 0x401F);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_swizzle((int)(uint32_t)(u >> 32), 0x401F);
+    v = v + __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+    v = v + dpp_shl_d(v, 8);
+    v = v + dpp_shl_d(v, 4);
+    v = v + dpp_shl_d(v, 2);
+    v = v + dpp_shl_d(v, 1);
+    return v;
+}
 __device__ __forceinline__ void rm_publish(const float (&part)[8], int k) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    float v[8];
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
-        float v = part[q];
+    for (int q = 0; q < 8; ++q) v[q] = rm_half_total(part[q]);
 #pragma unroll
-        for (int o = 16; o >= 1; o >>= 1) v = v + __shfl_xor(v, o, 64);
-        if ((lane & 31) == 0) s_red[k][wave][mfma_env(q, lane)] = v;
-    }
+    for (int q = 0; q < 8; ++q)
+        if ((lane & 31) == 0) s_red[k][wave][mfma_env(q, lane)] = v[q];
 }
 __device__ __forceinline__ void rm_publish_d(const double (&part)[8], int k) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    double v[8];
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
-        double v = part[q];
+    for (int q = 0; q < 8; ++q) v[q] = rm_half_total_d(part[q]);
 #pragma unroll
-        for (int o = 16; o >= 1; o >>= 1) v = v + __shfl_xor(v, o, 64);
-        if ((lane & 31) == 0) s_redd[k][wave][mfma_env(q, lane)] = v;
-    }
+    for (int q = 0; q < 8; ++q)
+        if ((lane & 31) == 0) s_redd[k][wave][mfma_env(q, lane)] = v[q];
 }
 __device__ __forceinline__ float rm_total(int e, int k) {
     float tot = 0.0f;
@@ -750,32 +790,34 @@ __device__ __forceinline__ const float* group_publish_x(const DevParams& p, Part
 // in RM order, samples stored by thread e.  RCX is a compile-time bound on the
 // rounds of a pass (register arrays); rounds past nk are skipped.
 template <int TPW, bool XL, int RCX>
-__device__ __forceinline__ void save_pass(const DevParams& p, const Slot& ws, int env_base, bool to_ring, Part& pt,
-                                          const float (&h)[8], int r0, int nrounds, bool gauss) {
+__device__ __forceinline__ void save_pass(const DevParams& __restrict__ p, const Slot& ws, int env_base, bool to_ring, Part& pt,
+                                          const float (&h)[8], int r0, int nrounds, bool gauss STAMP_PARAMS) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, tid = threadIdx.x;
     const int NG = XL ? __builtin_amdgcn_readfirstlane(pt.ng) : TPW * 256;
     const int col0 = XL ? __builtin_amdgcn_readfirstlane(pt.col0) : 0;
     const int nk = nrounds - r0 < RCX ? nrounds - r0 : RCX;
+    const int Bn = p.B;
     // per-round flag bits, 3 per round: LFP rows, and LFP or final rows
     constexpr int kLfp = (int)(02222222222u & ((1u << (3 * RCX)) - 1u));
     constexpr int kEval = (int)(06666666666u & ((1u << (3 * RCX)) - 1u));
-    if (tid < E_WG) {
-        const CtlE& c = s_ctl[tid];
-        for (int k = 0; k < RCX; ++k) {
-            const int r = r0 + k;
-            int fl = 0;
-            float th = 0.0f;
-            if (r < c.nsave) {
-                const int si = c.si + r;
-                const float ts = (float)grid_at_c(c, si);
-                th = (ts - c.tprev) / (c.tnext - c.tprev);
-                fl = 1 | ((si >= c.lfp_from && si < c.lfp_to) ? 2 : 0) | ((si == c.n - 1) ? 4 : 0);
-            }
-            s_theta[tid][k] = th;
-            s_rflag[tid][k] = fl;
+    // (1) abscissa and flags of every (env, round) of the pass: one thread each
+    if (tid < E_WG * RCX) {
+        const int e = tid % E_WG, k = tid / E_WG;
+        const CtlE& c = s_ctl[e];
+        const int r = r0 + k;
+        int fl = 0;
+        float th = 0.0f;
+        if (r < c.nsave) {
+            const int si = c.si + r;
+            const float ts = (float)grid_at_c(c, si);
+            th = (ts - c.tprev) / (c.tnext - c.tprev);
+            fl = 1 | ((si >= c.lfp_from && si < c.lfp_to) ? 2 : 0) | ((si == c.n - 1) ? 4 : 0);
         }
+        s_theta[e][k] = th;
+        s_rflag[e][k] = fl;
     }
     lds_barrier();
+    STAMP(11);
     float th[RCX][8];
     int fl[8];
     int anyl = 0;
@@ -809,6 +851,11 @@ __device__ __forceinline__ void save_pass(const DevParams& p, const Slot& ws, in
     constexpr int kSave = (int)(01111111111u & ((1u << (3 * RCX)) - 1u));
     const bool capture = p.rows != nullptr && !to_ring;
     const bool eval_rows = __any(flor & (capture ? kSave : kEval));  // rows to evaluate in any round
+    int fin = 0;  // wave-uniform: rounds holding some env's final row (bit k)
+#pragma unroll
+    for (int k = 0; k < RCX; ++k) fin |= __any((flor >> (3 * k)) & 4) ? (1 << k) : 0;
+    float* const yout = p.y;
+    float* const rows = p.rows;
     int rbase[8];  // captured row index of round 0 of this pass: sol_state_ row si - lfp_from + pos0
     if (capture) {
 #pragma unroll
@@ -817,6 +864,10 @@ __device__ __forceinline__ void save_pass(const DevParams& p, const Slot& ws, in
             rbase[q] = c.si + r0 - c.lfp_from + c.pos0;
         }
     }
+    // (2) dense output + LFP partials: every (round, env) of a tile is
+    // evaluated without branching (rows that are not saved or feed no LFP
+    // sample are computed and discarded by a select: the partial sums see
+    // exactly the additions of the branchy form, in the same order)
 #pragma unroll 1
     for (int t = 0; t < (eval_rows ? TPW : 0); ++t) {
         const int i = 32 * (wave * TPW + t) + (lane & 31);
@@ -831,34 +882,51 @@ __device__ __forceinline__ void save_pass(const DevParams& p, const Slot& ws, in
 #pragma unroll
             for (int q = 0; q < 8; ++q) {
                 int env = env_base + mfma_env(q, lane);
-                env = env < p.B ? env : p.B - 1;
+                env = env < Bn ? env : Bn - 1;
                 G[q] = p.g_rec[(size_t)env * NG + col0 + i];
             }
         }
+#ifdef KURA_STAMPS
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // attribute the record-load wait (diagnostic build)
+        STAMP(12);
+#endif
+        float k0[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) k0[q] = h[q] * f0[q];
 #pragma unroll
         for (int k = 0; k < RCX; ++k) {
             if (k >= nk) break;  // wave-uniform: past every env's last save of this step
+            float v[8];
 #pragma unroll
             for (int q = 0; q < 8; ++q) {
                 const int f = fl[q] >> (3 * k);
-                if (!(f & 1)) continue;
-                const float k0 = h[q] * f0[q];
                 const float x = th[k][q];
-                float v = ca[q] * x + cb[q];
-                v = v * x + cc[q];
-                v = v * x + k0;
-                v = v * x + y0[q];
-                if (f & 2) {
-                    const float cr = kdm_cosf(v);
-                    pn[k][q] = pn[k][q] + cr;
-                    if (gauss) pg[k][q] = pg[k][q] + (double)cr * G[q];
+                float w = ca[q] * x + cb[q];
+                w = w * x + cc[q];
+                w = w * x + k0[q];
+                w = w * x + y0[q];
+                v[q] = w;
+                const float cr = kdm_cosf(w);
+                pn[k][q] = (f & 2) ? pn[k][q] + cr : pn[k][q];
+                if (gauss) pg[k][q] = (f & 2) ? pg[k][q] + (double)cr * G[q] : pg[k][q];
+            }
+            if ((fin >> k) & 1) {  // the solve's last row: the new state
+#pragma unroll
+                for (int q = 0; q < 8; ++q) {
+                    const int env = env_base + mfma_env(q, lane);
+                    if (((fl[q] >> (3 * k)) & 4) && env < Bn) yout[(size_t)env * NG + col0 + i] = v[q];
                 }
-                const int env = env_base + mfma_env(q, lane);
-                if ((f & 4) && env < p.B) p.y[(size_t)env * NG + col0 + i] = v;
-                if (capture && env < p.B)
-                    p.rows[((size_t)env * (KURA_S_MAX + 1) + rbase[q] + k) * NG + col0 + i] = v;
+            }
+            if (capture) {
+#pragma unroll
+                for (int q = 0; q < 8; ++q) {
+                    const int env = env_base + mfma_env(q, lane);
+                    if (((fl[q] >> (3 * k)) & 1) && env < Bn)
+                        rows[((size_t)env * (KURA_S_MAX + 1) + rbase[q] + k) * NG + col0 + i] = v[q];
+                }
             }
         }
+        STAMP(13);
     }
 #pragma unroll
     for (int k = 0; k < RCX; ++k) {
@@ -869,41 +937,60 @@ __device__ __forceinline__ void save_pass(const DevParams& p, const Slot& ws, in
     }
     (void)anyw;
     lds_barrier();
-    float ltot[RCX];
-    double ltot_d[RCX];
-#pragma unroll
-    for (int k = 0; k < RCX; ++k) {
-        ltot[k] = 0.0f;
-        ltot_d[k] = 0.0;
-        if (tid < E_WG && (s_rflag[tid][k] & 2)) {
-            ltot[k] = rm_total(tid, k);
-            if (gauss) ltot_d[k] = rm_total_d(tid, k);
+    STAMP(14);
+    // (3) per (env, round) totals in wave order, LFP samples out
+    if constexpr (!XL) {
+        if (tid < E_WG * RCX) {
+            const int e = tid % E_WG, k = tid / E_WG;
+            if (s_rflag[e][k] & 2) {
+                const CtlE& c = s_ctl[e];
+                const float ln = rm_total(e, k) / (float)NG;
+                const double lr = gauss ? 0.0 + rm_total_d(e, k) / (double)NG : (double)ln;
+                const int pos = c.si + r0 + k - c.lfp_from + c.pos0;
+                if (to_ring) {
+                    p.ring[(size_t)(env_base + e) * p.W + pos] = lr;
+                } else {
+                    s_smp_n[e][pos] = ln;
+                    s_smp_r[e][pos] = lr;
+                }
+            }
         }
-    }
-    if constexpr (XL) {
-        if (__builtin_amdgcn_readfirstlane(anyw) & kLfp) group_sum<RCX>(p, pt, ltot, ltot_d, RCX, gauss);
-    }
-    if (tid < E_WG) {
-        const CtlE& c = s_ctl[tid];
+    } else {
+        float ltot[RCX];
+        double ltot_d[RCX];
+#pragma unroll
         for (int k = 0; k < RCX; ++k) {
-            if (!(s_rflag[tid][k] & 2)) continue;
-            const int si = c.si + r0 + k;
-            const float ln = ltot[k] / (float)NG;
-            const double lr = gauss ? 0.0 + ltot_d[k] / (double)NG : (double)ln;
-            const int pos = si - c.lfp_from + c.pos0;
-            if (to_ring) {
-                if (!XL || pt.part == 0) p.ring[(size_t)(env_base + tid) * p.W + pos] = lr;
-            } else {
-                s_smp_n[tid][pos] = ln;
-                s_smp_r[tid][pos] = lr;
+            ltot[k] = 0.0f;
+            ltot_d[k] = 0.0;
+            if (tid < E_WG && (s_rflag[tid][k] & 2)) {
+                ltot[k] = rm_total(tid, k);
+                if (gauss) ltot_d[k] = rm_total_d(tid, k);
+            }
+        }
+        if (__builtin_amdgcn_readfirstlane(anyw) & kLfp) group_sum<RCX>(p, pt, ltot, ltot_d, RCX, gauss);
+        if (tid < E_WG) {
+            const CtlE& c = s_ctl[tid];
+            for (int k = 0; k < RCX; ++k) {
+                if (!(s_rflag[tid][k] & 2)) continue;
+                const int si = c.si + r0 + k;
+                const float ln = ltot[k] / (float)NG;
+                const double lr = gauss ? 0.0 + ltot_d[k] / (double)NG : (double)ln;
+                const int pos = si - c.lfp_from + c.pos0;
+                if (to_ring) {
+                    if (pt.part == 0) p.ring[(size_t)(env_base + tid) * p.W + pos] = lr;
+                } else {
+                    s_smp_n[tid][pos] = ln;
+                    s_smp_r[tid][pos] = lr;
+                }
             }
         }
     }
     lds_barrier();
+    STAMP(15);
 }
 
 template <int TPW, bool XL>
-__device__ __forceinline__ void post_step(const DevParams& p, const Slot& ws, int env_base, bool to_ring, Part& pt
+__device__ __forceinline__ void post_step(const DevParams& __restrict__ p, const Slot& ws, int env_base, bool to_ring, Part& pt
                                           STAMP_PARAMS) {
     const int lane = threadIdx.x & 63, tid = threadIdx.x;
     const int NG = XL ? __builtin_amdgcn_readfirstlane(pt.ng) : TPW * 256;   // oscillators per env
@@ -1005,11 +1092,12 @@ __device__ __forceinline__ void post_step(const DevParams& p, const Slot& ws, in
     const bool gauss = p.rec_kernel == KURA_REC_GAUSSIAN;
     if (XL || gauss) {
 #pragma unroll 1
-        for (int r0 = 0; r0 < nrounds; r0 += RC) save_pass<TPW, XL, RC>(p, ws, env_base, to_ring, pt, h, r0, nrounds, gauss);
+        for (int r0 = 0; r0 < nrounds; r0 += RC)
+            save_pass<TPW, XL, RC>(p, ws, env_base, to_ring, pt, h, r0, nrounds, gauss STAMP_ARGS);
     } else {
 #pragma unroll 1
         for (int r0 = 0; r0 < nrounds; r0 += RC_N)
-            save_pass<TPW, XL, RC_N>(p, ws, env_base, to_ring, pt, h, r0, nrounds, false);
+            save_pass<TPW, XL, RC_N>(p, ws, env_base, to_ring, pt, h, r0, nrounds, false STAMP_ARGS);
     }
     STAMP(8);
     // (4) accepted envs: y0 <- y1, f0 <- f6 (FSAL)
@@ -1058,7 +1146,7 @@ __device__ __forceinline__ void post_step(const DevParams& p, const Slot& ws, in
 // One diffeqsolve for the workgroup's 16 envs.  s_ctl must be initialised
 // (ctl_begin) and visible before the call.
 template <int TPW, bool XL>
-__device__ void solve_wg(const DevParams& p, float* Xs, int env_base, bool to_ring, bool pulse_on,
+__device__ void solve_wg(const DevParams& __restrict__ p, float* Xs, int env_base, bool to_ring, bool pulse_on,
                          long long* rhs_count, Part& pt) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, tid = threadIdx.x;
     constexpr int N = TPW * 256;            // oscillators owned by this workgroup

@@ -15,7 +15,8 @@ import __graft_entry__ as ge  # noqa: E402
 
 LIB = os.path.join(ge.CSRC, "libkura_stamps.so")
 PHASES = ["stage_input", "barrier1", "gemm", "epilogue", "barrier2", "post_err", "flag_sync", "post_decide",
-          "post_saves", "post_fsal", "post_time", "gemm_p2", "hooks", "s13", "s14", "s15"]
+          "post_saves", "post_fsal", "post_time", "save_setup", "save_loadwait", "save_compute", "save_publish",
+          "save_totals"]
 
 
 def main():

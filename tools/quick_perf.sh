@@ -1,0 +1,9 @@
+# stamps (reset + step), bench, parity subset -- one gpurun call
+set -e
+O=gpurun_out/qp
+mkdir -p $O
+MODE=reset timeout -k 10 200 python3 -u tools/phase_stamps.py > $O/stamps_reset.json 2>/dev/null
+timeout -k 10 200 python3 -u tools/phase_stamps.py > $O/stamps_step.json 2>/dev/null
+timeout -k 10 300 python3 bench.py --steps 20 --warmup 3 --cpu-seconds 0 > $O/bench.json 2>$O/bench.err
+timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_configs.py tests/test_gpu_split.py -x -q --timeout 200 --timeout-method thread > $O/tests.log 2>&1 || (tail -30 $O/tests.log; exit 1)
+tail -2 $O/tests.log
