@@ -271,9 +271,8 @@ __device__ __forceinline__ void coupling_gemm(const float* __restrict__ Xs, cons
 // outstanding global store and load (vmcnt(0)) -- is not needed there; only
 // LDS (the GEMM operand, control slots, reduction partials) is shared.
 __device__ __forceinline__ void lds_barrier() {
-    // compiler-only barrier for the records: they are stored through global
-    // pointers and loaded through a buffer descriptor, and nothing may be
-    // reordered across a phase boundary
+    // compiler-only barrier for the records (buffer loads/stores through the
+    // workgroup's descriptor): nothing may be reordered across a phase boundary
     asm volatile("" ::: "memory");
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
     __builtin_amdgcn_s_barrier();
@@ -454,7 +453,6 @@ struct Slot {
     int N;
     int ct0;   // first column tile of this wave (wave * TPW), wave-uniform
     int voff;  // lane * 16 bytes (half 0); half 1 at +1024
-    gfloat* base;
     __device__ int soff(int slot, int t) const { return (slot * N + 32 * (ct0 + t)) * 64; }
 };
 
@@ -470,19 +468,16 @@ __device__ __forceinline__ void load8(const Slot& w, int slot, int t, float (&v)
     split8(a, b, v);
 }
 __device__ __forceinline__ void store8(const Slot& w, int slot, int t, const float (&v)[8]) {
-    // global stores with an SGPR base (slot/tile folded in by SALU) and the
-    // 32-bit lane offset.  Raw buffer stores are NOT used here: at N=256
-    // (one column tile per wave) they intermittently lost record components
-    // on gfx950 (ROCm 7.2), see DESIGN.md "Kernel notes".
+    // raw buffer stores through the same wave-uniform descriptor as the
+    // loads.  Every record is written and read back only by the lane that owns
+    // it, and one wave's vector-memory operations complete in issue order, so
+    // no wait is needed between a record store and a later load of it.
+    // (Round 1 used global stores here after an unexplained record loss at
+    // N=256 during development; it does not reproduce at the commit that
+    // introduced the workaround or at any later one)
     const floatx4 a = {v[0], v[1], v[2], v[3]}, b = {v[4], v[5], v[6], v[7]};
-#ifdef KURA_BUFSTORE  // diagnostic build: the raw buffer store form (tools/parity_probe.py)
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u32, a), w.rs, w.voff, w.soff(slot, t), 0);
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u32, b), w.rs, w.voff + 1024, w.soff(slot, t), 0);
-    return;
-#endif
-    __attribute__((address_space(1))) char* sb = (__attribute__((address_space(1))) char*)w.base + w.soff(slot, t);
-    *(gfx4*)(sb + (uint32_t)w.voff) = a;
-    *(gfx4*)(sb + (uint32_t)(w.voff + 1024)) = b;
 }
 
 // f = fmaf(kn, fmaf(c, P, -(s*Q)), omega) + pulse  ->  slot F0 + stage
@@ -1156,8 +1151,7 @@ __device__ void solve_wg(const DevParams& __restrict__ p, float* Xs, int env_bas
     const int pair = __builtin_amdgcn_readfirstlane(pt.pair);
     const Slot ws{__builtin_amdgcn_make_buffer_rsrc((void*)uniform_ptr(p.R + (size_t)pair * NSLOT * N * 16), 0,
                                                     NSLOT * N * 16 * 4, 0x00020000),
-                  N, wv * TPW, lane * 16,
-                  (gfloat*)uniform_ptr(p.R + (size_t)pair * NSLOT * N * 16)};
+                  N, wv * TPW, lane * 16};
     // records y0 <- state y, omega, pulse (0 while stimulation is OFF, env.py:434)
 #pragma unroll 1
     for (int t = 0; t < TPW; ++t) {

@@ -1,12 +1,10 @@
-# round-2 diagnostics (run via gpurun): buffer-store variant vs production on
-# the N=256 parity probe, phase stamps of reset and step, L2 hit/miss passes.
+# round-2 diagnostics (run via gpurun): phase stamps of reset and step, L2
+# hit/miss pass of the bench.
 set -e
 R=${GRAFT_REPO_ROOT:-$(pwd)}
-O=$R/gpurun_out/diag_a
+O=$R/gpurun_out/${1:-diag_a}
 mkdir -p $O
 cd $R
-timeout -k 10 150 python3 -u tools/parity_probe.py env0 256 16 10 rand $R/dbs-gym_amd/csrc/libkura_bufstore.so > $O/probe_bufstore.txt 2>&1
-timeout -k 10 150 python3 -u tools/parity_probe.py env0 256 16 10 rand > $O/probe_prod.txt 2>&1
 MODE=reset timeout -k 10 200 python3 -u tools/phase_stamps.py > $O/stamps_reset.json 2> $O/stamps_reset.err
 timeout -k 10 200 python3 -u tools/phase_stamps.py > $O/stamps_step.json 2> $O/stamps_step.err
 cd /tmp && export TMPDIR=/tmp
