@@ -1,6 +1,6 @@
 # stamps (reset + step), bench, parity subset -- one gpurun call
 set -e
-O=gpurun_out/qp
+O=gpurun_out/${1:-qp}
 mkdir -p $O
 MODE=reset timeout -k 10 200 python3 -u tools/phase_stamps.py > $O/stamps_reset.json 2>/dev/null
 timeout -k 10 200 python3 -u tools/phase_stamps.py > $O/stamps_step.json 2>/dev/null
