@@ -38,9 +38,17 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="env0", choices=["env0", "env1", "env2"])
     ap.add_argument("--osc", type=int, default=1024)
-    ap.add_argument("--envs", type=int, default=4096, help="envs per GPU")
+    ap.add_argument("--envs", type=int, default=4096, help="envs per GPU (weak scaling)")
+    ap.add_argument("--global-envs", type=int, default=0,
+                    help="total envs over all ranks (strong scaling: each rank owns global/world of them)")
+    ap.add_argument("--episode", action="store_true",
+                    help="also run one whole episode through KuraVectorEnv (autoreset included) -> extra.episode")
+    ap.add_argument("--episode-steps", type=int, default=0, help="episode length for --episode (0 = the config's)")
+    ap.add_argument("--episode-metrics", action="store_true",
+                    help="--episode with episode_metrics=True (beta power + envelope of every finished episode)")
     ap.add_argument("--reward", default="bbpow_action")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline sample (0 = skip)")
+    ap.add_argument("--cpu-seconds", type=float, default=24.0,
+                    help="bounded CPU-baseline budget in seconds (0 = skip), split over its legs")
     ap.add_argument("--seed", type=int, default=2024)
     ap.add_argument("--random-k", action="store_true", help="per-env K ~ U(0.3, 0.8) (north_star 'random K')")
     return ap.parse_args()
@@ -91,21 +99,95 @@ def _time_oracle(args, cfg, alpha, omega, g_stim, g_rec, theta0, ctab, stab, gai
     return nb * k / el, k, el
 
 
-def cpu_baseline(args, cfg, alpha, omega, g_stim, g_rec, theta0, ctab, stab, gain):
-    """The oracle (CPU restatement of step()) on this host's cores, bounded sample:
-    all cores (one env per OpenMP thread) and, beside it, one core (one env)."""
+def _host_cores():
     ncores = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
-    nthreads = int(os.environ.get("OMP_NUM_THREADS", ncores))
+    return int(os.environ.get("OMP_NUM_THREADS", ncores))
+
+
+def cpu_oracle_c(args, cfg, alpha, omega, g_stim, g_rec, theta0, ctab, stab, gain, seconds):
+    """The bit-exact C oracle (factorised RHS, the HIP path's twin) on this
+    host's cores: all cores (one env per OpenMP thread) and one core."""
+    nthreads = _host_cores()
     nb = max(1, min(nthreads, cfg.n_envs))
     arrs = (args, cfg, alpha, omega, g_stim, g_rec, theta0, ctab, stab, gain)
-    v, k, el = _time_oracle(*arrs, nb, args.cpu_seconds)
-    v1, k1, el1 = _time_oracle(*arrs, 1, max(1.0, args.cpu_seconds / 3))
-    return {"value": v, "unit": "env-steps/s", "cores": nthreads, "kind": "port",
-            "sample": f"oracle/kura_oracle.c (CPU restatement of step(), bit-exact twin of the HIP path), "
-                      f"{args.config} N={cfg.n_osc}, {nb} envs x {k} steps after reset, {el:.1f} s, "
-                      f"OpenMP {nthreads} threads (one env per thread)",
-            "single_core_value": v1,
-            "single_core_sample": f"1 env x {k1} steps, {el1:.1f} s, one thread"}
+    v, k, el = _time_oracle(*arrs, nb, seconds)
+    v1, k1, el1 = _time_oracle(*arrs, 1, max(1.0, seconds / 3))
+    return {"value": v, "cores": nthreads, "single_core_value": v1,
+            "sample": f"oracle/kura_oracle.c, {args.config} N={cfg.n_osc}, {nb} envs x {k} steps ({el:.1f} s, OpenMP "
+                      f"{nthreads} threads) and 1 env x {k1} steps ({el1:.1f} s)"}
+
+
+_REF_ENV = None
+
+
+def _ref_child(seconds):
+    """(forked worker) steps/s of the reference-op-sequence env prepared by the parent."""
+    from oracle.ref_numpy import time_steps
+    v, k, el = time_steps(_REF_ENV, seconds, np.random.default_rng(os.getpid()))
+    return v, k
+
+
+def _ref_env(args, n_osc):
+    """env 0 of the bench's workload at n_osc oscillators as an oracle/ref_numpy.RefOpEnv, started from the
+    state reset() leaves (the transient is run by the C oracle: ~460 direct-sin RHS at N=1024 would take
+    ~5 s per process)."""
+    from oracle import kura_oracle as ko
+    from oracle.ref_numpy import RefOpEnv
+    import copy
+    a = copy.copy(args)
+    a.osc, a.envs, a.random_k = n_osc, 1, False
+    cfg, alpha, omega, gs, gr, th0, ct, st, gain = build_shard(a, 0)
+    o = ko.Oracle(cfg, alpha)
+    o.set_env_params(omega, gs, gr)
+    o.set_spectral(ct, st)
+    o.reset(th0)
+    state = o.state()
+    o.close()
+    env = RefOpEnv(alpha, omega[0], gs[0], K=float(gain[0]) * n_osc if gain is not None else 0.52,
+                   W=cfg.window, dbs_bounds=(cfg.dbs_lo, cfg.dbs_hi))
+    env.sol = state["y"][0][None, :].astype(np.float32)
+    env.t = float(state["t"][0])
+    wp = int(state["wpos"][0])
+    env.window = np.roll(state["ring"][0], -wp)
+    return env
+
+
+def cpu_baseline(args):
+    """the reference's step() op sequence (direct N^2
+    sin coupling, oracle/ref_numpy.py) on this host's cores, bounded samples,
+    measured before this process touches the GPU (the all-cores leg forks):
+      value        all cores, one env per process, N = the bench's N (1024);
+      single_core  one core, same N;
+      n512         one core at the reference configs' N=512 (the published
+                   JAX-CPU notebook rate is 16.96-19.77 steps/s, BASELINE.md 1);
+      oracle_c     the bit-exact C oracle (factorised RHS), all cores / one core."""
+    import multiprocessing as mp
+    global _REF_ENV
+    sec = args.cpu_seconds
+    nproc = _host_cores()
+    out = {"unit": "env-steps/s", "kind": "port"}
+    _REF_ENV = _ref_env(args, args.osc)
+    from oracle.ref_numpy import time_steps
+    v1, k1, el1 = time_steps(_REF_ENV, sec / 3)
+    ctx = mp.get_context("fork")
+    t0 = time.perf_counter()
+    with ctx.Pool(nproc) as pool:
+        res = pool.map(_ref_child, [sec / 3] * nproc)
+    el = time.perf_counter() - t0
+    out["value"] = float(sum(v for v, _ in res))
+    out["cores"] = nproc
+    out["sample"] = (f"oracle/ref_numpy.py (reference op sequence: fmod + direct N^2 sin coupling, env.py:252-256; "
+                     f"Dopri5/PID/dense output; R1), {args.config} N={args.osc}: {nproc} processes x 1 env, "
+                     f"{sum(k for _, k in res)} steps in {el:.1f} s wall, started from the reset() state")
+    out["single_core_value"] = v1
+    out["single_core_sample"] = f"1 env x {k1} steps, {el1:.1f} s, one core"
+    if args.osc != 512:
+        _REF_ENV = _ref_env(args, 512)
+        v5, k5, el5 = time_steps(_REF_ENV, sec / 4)
+        out["n512_single_core_value"] = v5
+        out["n512_sample"] = f"N=512 reference env0 config, 1 env x {k5} steps, {el5:.1f} s, one core"
+    _REF_ENV = None
+    return out
 
 
 def kernel_name(N):
@@ -134,6 +216,60 @@ def pmc_traffic(N, B):
         return None, None, None
 
 
+def episode_bench(args, rank, world, local_rank):
+    """One whole episode of B envs through the drop-in KuraVectorEnv: every
+    step() of the episode plus the autoreset at its end (host reset draws,
+    parameter upload, masked reset kernel; with --episode-metrics the
+    per-episode beta power and envelope statistics).  Returns the
+    episode-inclusive rate beside the breakdown of the episode boundary."""
+    import torch
+    import torch.distributed as dist
+    kura = importlib.import_module("dbs-gym_amd")
+    vec = importlib.import_module("dbs-gym_amd.vec_env")
+    base = kura.synthetic_params(args.config, args.osc) if args.osc != 512 else kura.reference_params(args.config)
+    if args.episode_steps:
+        base["total_episode_len"] = args.episode_steps * (base["electrode_width"] + base["electrode_pause"])
+    B = args.envs
+    plist = []
+    for b in range(B):
+        gid = rank * B + b
+        p = dict(base)
+        p["rand_seed"] = args.seed + gid
+        if args.random_k:
+            p["K"] = float(np.random.default_rng(args.seed * 7919 + gid).uniform(0.3, 0.8))
+        plist.append(p)
+    t0 = time.perf_counter()
+    env = vec.KuraVectorEnv(plist, device=local_rank, reward_func=args.reward, w0_seed=10_000_000 + args.seed + rank * B,
+                            episode_metrics=args.episode_metrics, profile=True)
+    setup_s = time.perf_counter() - t0
+    dev = env.device
+    env.reset()
+    L = int(env.episode_steps)
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(args.seed + 7 * rank + 1)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for k in range(L):
+        env.step(torch.rand((B, 1), generator=gen, device=dev) * 2 - 1)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    bt = env.boundary_times[-1] if env.boundary_times else {}
+    env.close()
+    return {"workload": f"one episode of {L} steps x {B} envs per GPU through KuraVectorEnv, autoreset of every env "
+                        f"at its end{' with episode metrics (bbpow + envelope)' if args.episode_metrics else ''}",
+            "episode_steps": L, "value": world * B * L / el, "unit": "env-steps/s", "episode_s": el,
+            "boundary": bt, "boundary_frac": (sum(v for k, v in bt.items() if k.endswith("_s")) / el) if bt else None,
+            "setup_s": setup_s}
+
+
 def main():
     args = parse()
     import torch
@@ -144,11 +280,18 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus and rank == 0:
         print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+    # CPU baseline first: the reference-op leg forks worker processes, which
+    # must happen before this process initialises the GPU
+    cpu = cpu_baseline(args) if (world == 1 and args.cpu_seconds > 0) else None
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
 
+    if args.global_envs:
+        if args.global_envs % world:
+            raise SystemExit(f"--global-envs {args.global_envs} is not a multiple of WORLD_SIZE={world}")
+        args.envs = args.global_envs // world
     sim_mod = importlib.import_module("dbs-gym_amd.sim")
     t_setup = time.perf_counter()
     cfg, alpha, omega, g_stim, g_rec, theta0, ctab, stab, gain = build_shard(args, rank)
@@ -217,7 +360,8 @@ def main():
         bytes_launch = B * bytes_env + 4 * N * N
         traffic, traffic_src, clock_ghz = pmc_traffic(N, B)
         out = {
-            "metric": f"env steps/sec (whole node), N={N} osc x {B} envs per GPU",
+            "metric": (f"env steps/sec (whole node), N={N} osc x {world * B} envs over {world} GPUs" if args.global_envs
+                       else f"env steps/sec (whole node), N={N} osc x {B} envs per GPU"),
             "value": value,
             "unit": "env-steps/s",
             "n_gpus": world,
@@ -225,7 +369,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": el_max / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if args.global_envs else "weak",
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic (seeded reference-sampler natural frequencies, N(pi,0.6) phases, U(-1,1) actions)",
@@ -251,12 +395,22 @@ def main():
                       "reset_ms": t_reset * 1e3, "reset_rhs_max": int(reset_stats[0]),
                       "host_setup_s": t_setup},
         }
-        if world == 1 and args.cpu_seconds > 0:
-            out["cpu_baseline"] = cpu_baseline(args, cfg, alpha, omega, g_stim, g_rec, theta0, ctab, stab, gain)
-        else:
-            out["cpu_baseline"] = None
+    if args.episode:
+        sim.close()
+        sim = None
+        ep = episode_bench(args, rank, world, local_rank)
+        if rank == 0:
+            ep["steady_state_value"] = out["value"]
+            ep["episode_vs_steady"] = ep["value"] / out["value"]
+            out["extra"]["episode"] = ep
+    if rank == 0:
+        if cpu is not None:
+            cpu["oracle_c"] = cpu_oracle_c(args, cfg, alpha, omega, g_stim, g_rec, theta0, ctab, stab, gain,
+                                           max(2.0, args.cpu_seconds / 2))
+        out["cpu_baseline"] = cpu
         print(json.dumps(out), flush=True)
-    sim.close()
+    if sim is not None:
+        sim.close()
     if world > 1:
         dist.destroy_process_group()
 

@@ -117,14 +117,28 @@ class EnvHost:
         w0 = ms.remove_negative_w0(self.rs, w0)                                # KuramotoJAX.__init__ env.py:213
         if np.min(w0) < 0:
             raise AssertionError("Natural frequencies w0 must be positive!")   # env.py:214
-        gs = p["grid_size"]
-        naive = p["naive_dbs"]
-        g_stim = ms.conductances(self.grid, gs, self.elec_coords, self.encapsulation_coeff, naive)
-        g_rec = ms.conductances(self.grid, gs, self.rec_coords, self.encapsulation_coeff, naive)
-        if p.get("directed_stimulation"):                                      # env.py:125-140
-            g_stim = ms.directed_conductances(self.grid, gs, self.elec_coords, g_stim)
+        g_stim, g_rec = self._conductances()
         theta0 = ms.initial_phases(self.rs, self.N, p["init_state_mean"], p["init_state_sd"])  # env.py:595-598
         return w0, g_stim, g_rec, theta0
+
+
+    def _conductances(self):
+        """SimpleDBS conductances of the current contacts (env.py:106-156).  They
+        depend only on the contacts and the encapsulation modifier, which change
+        only at drift / spatial-variation events, so the last result is reused
+        until one of them changes (returned read-only)."""
+        key = (repr(self.elec_coords), repr(self.rec_coords), float(self.encapsulation_coeff))
+        if getattr(self, "_g_key", None) != key:
+            p = self.p
+            gs, naive = p["grid_size"], p["naive_dbs"]
+            g_stim = ms.conductances(self.grid, gs, self.elec_coords, self.encapsulation_coeff, naive)
+            g_rec = ms.conductances(self.grid, gs, self.rec_coords, self.encapsulation_coeff, naive)
+            if p.get("directed_stimulation"):                                  # env.py:125-140
+                g_stim = ms.directed_conductances(self.grid, gs, self.elec_coords, g_stim)
+            g_stim.setflags(write=False)
+            g_rec.setflags(write=False)
+            self._g_key, self._g = key, (g_stim, g_rec)
+        return self._g
 
 
 def fill_driver_arrays(params: dict, w0_seed: int | None = None, rs: np.random.RandomState | None = None) -> dict:

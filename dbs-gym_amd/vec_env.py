@@ -14,6 +14,7 @@ torch tensors unless the caller asks for NumPy.
 from __future__ import annotations
 
 import copy
+import time
 
 import numpy as np
 import torch
@@ -53,6 +54,9 @@ class KuraVectorEnv:
     autoreset:  SB3 DummyVecEnv semantics -- a finished env is reset inside the
                 same step() and its last observation is returned in
                 ``infos["terminal_observation"]``.
+    profile:    time the phases of every autoreset (host draws, parameter
+                upload, reset kernel, episode metrics; synchronising) into
+                ``self.boundary_times`` -- bench.py --episode.
     on_failure: a solve that fails inside the library (kura.h KURA_F_*:
                 max_steps, non-finite state, ...) -- "raise" (default) raises
                 KuraSolverError from step()/reset(), as the reference's
@@ -67,10 +71,12 @@ class KuraVectorEnv:
     def __init__(self, params, num_envs: int | None = None, device=0, reward_func: str | None = None,
                  w0_seed: int = 228, rand_seeds=None, autoreset: bool = True, max_steps: int = 4096,
                  episode_metrics: bool = False, psd_dt: float = 5e-4, beta_band=(12.5, 21.0),
-                 on_failure: str = "raise"):
+                 on_failure: str = "raise", profile: bool = False):
         if on_failure not in ("raise", "reset"):
             raise ValueError(f"on_failure={on_failure!r}: expected 'raise' or 'reset'")
         self.on_failure = on_failure
+        self.profile = profile
+        self.boundary_times: list[dict] = []
         if isinstance(params, dict):
             if num_envs is None:
                 raise ValueError("num_envs is required with a single params dict")
@@ -120,6 +126,7 @@ class KuraVectorEnv:
         """Host draws of reset() for the envs in idx; uploads only their
         parameters (one kura_set_env_params per contiguous run of envs)."""
         idx = sorted(int(b) for b in idx)
+        t0 = time.perf_counter()
         th = np.zeros((self.num_envs, self.N), np.float32)
         for b in idx:
             w0, gs, gr, th0 = self.hosts[b].reset_draws()
@@ -127,6 +134,7 @@ class KuraVectorEnv:
             self._g_stim[b] = gs
             self._g_rec[b] = gr
             th[b] = th0.astype(np.float32)
+        self._t_draw = time.perf_counter() - t0
         k = 0
         while k < len(idx):
             j = k
@@ -135,7 +143,11 @@ class KuraVectorEnv:
             a, b = idx[k], idx[j] + 1
             self.sim.set_env_params(self._omega[a:b], self._g_stim[a:b], self._g_rec[a:b], env0=a)
             k = j + 1
-        return torch.from_numpy(th).to(self.device)
+        out = torch.from_numpy(th).to(self.device)
+        if self.profile:
+            torch.cuda.synchronize(self.device)
+        self._t_upload = time.perf_counter() - t0 - self._t_draw
+        return out
 
     def reset(self, seed=None, options=None):
         """env.py:467-614 for every env.  ``seed`` (int or list) reseeds the
@@ -175,7 +187,9 @@ class KuraVectorEnv:
             truncated[torch.as_tensor(failed, device=self.device)] = True
             term_host = term_host.copy()
             term_host[failed] = True                     # autoreset keys on the same envs the flags name
+        tb = {}
         if term_host.any():
+            t0 = time.perf_counter()
             idx = np.nonzero(term_host)[0]
             infos["terminal_env_ids"] = idx
             infos["episode"] = {"l": self.steps[idx].copy()}
@@ -187,14 +201,22 @@ class KuraVectorEnv:
                 # per_episode/envelope/{mean,std,cum} of the training callback (custom_callbacks.py:146-148)
                 ev = self.sim.episode_envelope_stats(mask)
                 infos["episode"]["envelope"] = ev[torch.as_tensor(idx, device=self.device)].cpu().numpy()
+            tb["metrics_s"] = time.perf_counter() - t0
         if self.autoreset and term_host.any():
             infos["terminal_observation"] = obs[torch.as_tensor(idx, device=self.device)].clone().view(-1, 1, self.W)
             mask = torch.zeros(self.num_envs, dtype=torch.uint8)
             mask[idx] = 1
             th = self._draw(idx)
+            t1 = time.perf_counter()
             self.sim.reset(th, mask.to(self.device))
             self._check_reset(mask)
+            if self.profile:
+                torch.cuda.synchronize(self.device)
             self.steps[idx] = 0
+            tb.update(n_reset=len(idx), host_draw_s=self._t_draw, upload_s=self._t_upload,
+                      reset_kernel_s=time.perf_counter() - t1)
+        if self.profile and tb:
+            self.boundary_times.append(tb)
         return obs.view(self.num_envs, 1, self.W).clone(), rew.clone(), terminated, truncated, infos
 
     def _check_reset(self, mask):
