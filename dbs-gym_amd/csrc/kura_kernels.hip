@@ -1800,150 +1800,7 @@ __global__ __launch_bounds__(64) void kura_reward_kernel(DevParams p, const doub
     if (lane == 0) out[env] = r;
 }
 
-// ------------------------------------------ episode metric (f) rank 3 ----
-// calc_psd_for_simple_eval (aDBS_RL/evaluate_HF_DBS.py:122-135) of one
-// signal per workgroup: band_pass_envelope's filtfilt (utils.py:794-816, the
-// R2 Butterworth; lane 0, scipy DF2T order), a direct DFT of the bins the
-// beta band and the 12-tap smoothing need (threads own contiguous sample
-// segments; exact start twiddle per segment + complex rotation), |X/n|^2*2,
-// filtfilt(ones(12), 5, .) evaluated on those bins (exact away from the
-// spectrum ends), and the sum over beta_a < f < beta_b.
-#define PSD_THREADS 256
-#define PSD_MAXB 2048
-#define PSD_HALO 12
-
-__device__ void filtfilt_full_dev(const DevParams& p, const float* x, int L, double* ext, double* tmp) {
-    const int P = p.padlen, M = L + 2 * P;
-    const double x0 = (double)x[0], xl = (double)x[L - 1];
-    for (int i = 0; i < P; ++i) ext[i] = 2.0 * x0 - (double)x[P - i];
-    for (int i = 0; i < L; ++i) ext[P + i] = (double)x[i];
-    for (int i = 0; i < P; ++i) ext[P + L + i] = 2.0 * xl - (double)x[L - 2 - i];
-    for (int pass = 0; pass < 2; ++pass) {
-        const double e0 = ext[0];
-        double z0 = p.bw_zi[0] * e0, z1 = p.bw_zi[1] * e0, z2 = p.bw_zi[2] * e0, z3 = p.bw_zi[3] * e0;
-        for (int k = 0; k < M; ++k) {
-            const double xn = ext[k];
-            const double yn = z0 + p.bw_b[0] * xn;
-            z0 = (z1 + xn * p.bw_b[1]) - yn * p.bw_a[1];
-            z1 = (z2 + xn * p.bw_b[2]) - yn * p.bw_a[2];
-            z2 = (z3 + xn * p.bw_b[3]) - yn * p.bw_a[3];
-            z3 = xn * p.bw_b[4] - yn * p.bw_a[4];
-            tmp[k] = yn;
-        }
-        if (pass == 0)
-            for (int i = 0; i < M; ++i) ext[i] = tmp[M - 1 - i];
-    }
-    for (int i = 0; i < L; ++i) ext[i] = tmp[M - 1 - P - i];
-}
-
-__global__ __launch_bounds__(PSD_THREADS) void kura_psd_kernel(DevParams p, const float* __restrict__ sig,
-                                                               const int* __restrict__ lens, long long ld, int j0,
-                                                               int n, int episode, const uint8_t* __restrict__ mask,
-                                                               double psd_dt, double beta_a, double beta_b,
-                                                               double* scratch, long long sld,
-                                                               double* __restrict__ out) {
-    __shared__ double s_ft[PSD_MAXB];
-    __shared__ double s_part[PSD_THREADS / 64][2];
-    const int j = j0 + blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    if (j >= n) return;
-    const double qnan = __builtin_nan("");
-    int L;
-    const float* x;
-    if (episode) {
-        L = p.ep_len[j];
-        x = p.ep_lfp + (size_t)j * p.episode_cap;
-        if ((mask && !mask[j]) || L > p.episode_cap || L < 2) {
-            if (tid == 0) out[j] = qnan;
-            return;
-        }
-    } else {
-        L = lens[j];
-        x = sig + (size_t)j * ld;
-        if (L < 2 || L > ld) {
-            if (tid == 0) out[j] = qnan;
-            return;
-        }
-    }
-    // band bins exactly as np.fft.rfftfreq: f_k = k * (1.0 / (L * psd_dt))
-    const int M = L / 2 + 1;
-    const double val = 1.0 / ((double)L * psd_dt);
-    int k0 = (int)(beta_a / val) - 2, k1 = (int)(beta_b / val) + 2;
-    k0 = k0 < 0 ? 0 : k0;
-    while (k0 < M && !((double)k0 * val > beta_a)) ++k0;
-    k1 = k1 > M - 1 ? M - 1 : k1;
-    while (k1 >= 0 && !((double)k1 * val < beta_b)) --k1;
-    if (k1 < k0) {
-        if (tid == 0) out[j] = 0.0;  // np.sum of an empty selection
-        return;
-    }
-    const int lo = k0 - PSD_HALO, hi = k1 + PSD_HALO, K = hi - lo + 1;
-    // the smoothing filtfilt's odd padding (36 bins) and its 11-bin transients
-    // must stay outside [lo, hi]
-    if (lo < 48 || hi > M - 49 || K > PSD_MAXB) {
-        if (tid == 0) out[j] = qnan;
-        return;
-    }
-    double* ext = scratch + (size_t)blockIdx.x * sld;
-    double* tmp = ext + sld / 2;
-    if (tid == 0) filtfilt_full_dev(p, x, L, ext, tmp);
-    __syncthreads();  // lane 0's global scratch stores are visible workgroup-wide after the barrier
-    const int seg = (L + PSD_THREADS - 1) / PSD_THREADS;
-    const int t0 = tid * seg, t1 = t0 + seg < L ? t0 + seg : L;
-    for (int kk = 0; kk < K; ++kk) {
-        const long long k = lo + kk;
-        double re = 0.0, im = 0.0;
-        if (t0 < t1) {
-            const long long m = (k * (long long)t0) % L;
-            double ws, wc, rs, rc;
-            sincos(-2.0 * M_PI * (double)m / (double)L, &ws, &wc);
-            sincos(-2.0 * M_PI * (double)k / (double)L, &rs, &rc);
-            for (int t = t0; t < t1; ++t) {
-                const double y = ext[t];
-                re = fma(y, wc, re);
-                im = fma(y, ws, im);
-                const double nc = wc * rc - ws * rs;
-                ws = wc * rs + ws * rc;
-                wc = nc;
-            }
-        }
-        re = wave_sum_f64(re);
-        im = wave_sum_f64(im);
-        if (lane == 0) {
-            s_part[wave][0] = re;
-            s_part[wave][1] = im;
-        }
-        __syncthreads();
-        if (tid == 0) {
-            double a = 0.0, b = 0.0;
-            for (int w = 0; w < PSD_THREADS / 64; ++w) {
-                a = a + s_part[w][0];
-                b = b + s_part[w][1];
-            }
-            const double h = hypot(a / (double)L, b / (double)L);
-            s_ft[kk] = h * h * 2.0;
-        }
-        __syncthreads();
-    }
-    if (tid == 0) {
-        // filtfilt(ones(12), 5, ft): b = 1/5 each (lfilter normalises by a[0]),
-        // forward then backward, DF2T association (oldest term innermost)
-        const double bb = 1.0 / 5.0;
-        double* yf = tmp;  // forward output, index kk
-        for (int kk = 11; kk < K; ++kk) {
-            double acc = bb * s_ft[kk - 11];
-            for (int q = 10; q >= 1; --q) acc = acc + bb * s_ft[kk - q];
-            yf[kk] = acc + bb * s_ft[kk];
-        }
-        double tot = 0.0;
-        for (int kk = k0 - lo; kk <= k1 - lo; ++kk) {
-            double acc = bb * yf[kk + 11];
-            for (int q = 10; q >= 1; --q) acc = acc + bb * yf[kk + q];
-            const double zs = acc + bb * yf[kk];
-            tot = tot + zs;
-        }
-        out[j] = tot;
-    }
-}
+#include "kura_fft.inc"
 
 // ------------------------------------------------------------- self-tests --
 __global__ void kura_selftest_math_kernel(const float* x, const float* y, float* out, int n) {
@@ -1982,173 +1839,6 @@ __global__ __launch_bounds__(NTHREADS) void kura_selftest_gemm_kernel(const floa
             const int col = 32 * (wave * TPW + t) + (lane & 31);
             Y[(size_t)row * N + col] = acc[t][q];
         }
-}
-
-// explicit instantiations are made by the launchers in kura_capi.hip
-// ---- episode envelope statistics (aDBS_RL/agents/custom_callbacks.py:146-148)
-// log_main_metrics('per_episode', 'envelope', calc_envelope(lfp_ep)):
-// calc_envelope = |scipy.signal.hilbert(x)| (environment/utils.py:835-836),
-// then mean, std(ddof=1) and sum (custom_callbacks.py:28-31).  Hilbert as
-// scipy does it: X = fft(x), X[k] *= h[k] (h = 1 at DC and, for even n, at
-// n/2; 2 on the positive bins; 0 on the negative ones), z = ifft.  Three
-// kernels per chunk of signals, float64 throughout, direct DFT with twiddles
-// exact (sincospi of (k*t mod n)/n) at each 1024/512-term tile start and
-// rotated inside it: O(n^2) work, compute bound;
-// an evaluation-time metric, not on the step path.
-#define ENV_THREADS 256
-#define ENV_TILE 1024
-
-__device__ __forceinline__ bool env_signal(const DevParams& p, const float* sig, const int* lens, long long ld,
-                                           int j, int episode, const uint8_t* mask, int& L, const float*& x) {
-    if (episode) {
-        L = p.ep_len[j];
-        x = p.ep_lfp + (size_t)j * p.episode_cap;
-        return !(mask && !mask[j]) && L >= 1 && L <= p.episode_cap;
-    }
-    L = lens[j];
-    x = sig + (size_t)j * ld;
-    return L >= 1 && L <= ld;
-}
-
-// analytic half-spectrum h[k]*X[k], k in [0, L/2]: one thread per bin,
-// signal tiles staged through LDS (float -> double once per tile)
-__global__ __launch_bounds__(ENV_THREADS) void kura_env_fwd_kernel(DevParams p, const float* __restrict__ sig,
-                                                                   const int* __restrict__ lens, long long ld,
-                                                                   int j0, int episode,
-                                                                   const uint8_t* __restrict__ mask,
-                                                                   double* scratch, long long sld) {
-    __shared__ double s_x[ENV_TILE];
-    const int j = j0 + blockIdx.y;
-    int L;
-    const float* x;
-    if (!env_signal(p, sig, lens, ld, j, episode, mask, L, x)) return;
-    const int nb = L / 2 + 1;
-    if ((int)(blockIdx.x * ENV_THREADS) >= nb) return;  // whole block idle (uniform)
-    const int k = blockIdx.x * ENV_THREADS + threadIdx.x;
-    const bool act = k < nb;
-    const long long kk = act ? k : 0;
-    const double inv = 2.0 / (double)L;
-    double re = 0.0, im = 0.0;
-    double ws, wc;  // per-sample rotation e^{-2 pi i k / L}
-    sincospi((double)kk * inv, &ws, &wc);
-    ws = -ws;
-    for (int t0 = 0; t0 < L; t0 += ENV_TILE) {
-        const int cnt = L - t0 < ENV_TILE ? L - t0 : ENV_TILE;
-        __syncthreads();
-        for (int i = threadIdx.x; i < cnt; i += ENV_THREADS) s_x[i] = (double)x[t0 + i];
-        __syncthreads();
-        // exact twiddle at the tile start, rotated within the tile (error
-        // growth ~ENV_TILE ulp, far inside the 1e-9 parity bar)
-        double cs, sn;
-        sincospi((double)((kk * t0) % L) * inv, &sn, &cs);
-        sn = -sn;
-        for (int i = 0; i < cnt; ++i) {
-            re = fma(s_x[i], cs, re);
-            im = fma(s_x[i], sn, im);
-            const double c2 = fma(cs, wc, -sn * ws);
-            sn = fma(cs, ws, sn * wc);
-            cs = c2;
-        }
-    }
-    if (act) {
-        const double h = (k == 0 || (L % 2 == 0 && k == L / 2)) ? 1.0 : 2.0;
-        double* X = scratch + (size_t)blockIdx.y * sld;
-        X[2 * k] = h * re;
-        X[2 * k + 1] = h * im;
-    }
-}
-
-// |z[t]| = |ifft(hX)[t]| for t in [0, L): one thread per sample, the half
-// spectrum staged through LDS
-__global__ __launch_bounds__(ENV_THREADS) void kura_env_inv_kernel(DevParams p, const float* __restrict__ sig,
-                                                                   const int* __restrict__ lens, long long ld,
-                                                                   int j0, int episode,
-                                                                   const uint8_t* __restrict__ mask,
-                                                                   double* scratch, long long sld) {
-    __shared__ double s_X[2 * (ENV_TILE / 2)];
-    const int j = j0 + blockIdx.y;
-    int L;
-    const float* x;
-    if (!env_signal(p, sig, lens, ld, j, episode, mask, L, x)) return;
-    if ((int)(blockIdx.x * ENV_THREADS) >= L) return;
-    const int nb = L / 2 + 1;
-    const int t = blockIdx.x * ENV_THREADS + threadIdx.x;
-    const bool act = t < L;
-    const long long tt = act ? t : 0;
-    const double inv = 2.0 / (double)L;
-    const double* X = scratch + (size_t)blockIdx.y * sld;
-    double re = 0.0, im = 0.0;
-    double ws, wc;  // per-bin rotation e^{+2 pi i t / L}
-    sincospi((double)tt * inv, &ws, &wc);
-    constexpr int TB = ENV_TILE / 2;
-    for (int k0 = 0; k0 < nb; k0 += TB) {
-        const int cnt = nb - k0 < TB ? nb - k0 : TB;
-        __syncthreads();
-        for (int i = threadIdx.x; i < 2 * cnt; i += ENV_THREADS) s_X[i] = X[2 * k0 + i];
-        __syncthreads();
-        double cs, sn;  // exact at the tile start, rotated within it
-        sincospi((double)(((long long)k0 * tt) % L) * inv, &sn, &cs);
-        for (int i = 0; i < cnt; ++i) {
-            const double a = s_X[2 * i], b = s_X[2 * i + 1];
-            re = fma(a, cs, re);
-            re = fma(-b, sn, re);
-            im = fma(a, sn, im);
-            im = fma(b, cs, im);
-            const double c2 = fma(cs, wc, -sn * ws);
-            sn = fma(cs, ws, sn * wc);
-            cs = c2;
-        }
-    }
-    if (act) {
-        double* E = scratch + (size_t)blockIdx.y * sld + 2 * (size_t)nb;
-        E[t] = hypot(re, im) / (double)L;
-    }
-}
-
-// out[3j..3j+2] = mean, std(ddof=1), sum of the envelope (fixed-order f64
-// reductions; NaN for unselected / out-of-range signals, std NaN for L == 1)
-__global__ __launch_bounds__(ENV_THREADS) void kura_env_stats_kernel(DevParams p, const float* __restrict__ sig,
-                                                                     const int* __restrict__ lens, long long ld,
-                                                                     int j0, int episode,
-                                                                     const uint8_t* __restrict__ mask,
-                                                                     const double* scratch, long long sld,
-                                                                     double* __restrict__ out) {
-    __shared__ double s_r[ENV_THREADS];
-    const int j = j0 + blockIdx.x, tid = threadIdx.x;
-    const double qnan = __builtin_nan("");
-    int L;
-    const float* x;
-    if (!env_signal(p, sig, lens, ld, j, episode, mask, L, x)) {
-        if (tid == 0) out[3 * j] = out[3 * j + 1] = out[3 * j + 2] = qnan;
-        return;
-    }
-    const double* E = scratch + (size_t)blockIdx.x * sld + 2 * (size_t)(L / 2 + 1);
-    auto block_sum = [&](double v) {
-        s_r[tid] = v;
-        __syncthreads();
-        for (int w = ENV_THREADS / 2; w > 0; w >>= 1) {
-            if (tid < w) s_r[tid] += s_r[tid + w];
-            __syncthreads();
-        }
-        const double r = s_r[0];
-        __syncthreads();
-        return r;
-    };
-    double a = 0.0;
-    for (int t = tid; t < L; t += ENV_THREADS) a += E[t];
-    const double sum = block_sum(a);
-    const double mean = sum / (double)L;
-    double q = 0.0;
-    for (int t = tid; t < L; t += ENV_THREADS) {
-        const double d = E[t] - mean;
-        q = fma(d, d, q);
-    }
-    const double ss = block_sum(q);
-    if (tid == 0) {
-        out[3 * j] = mean;
-        out[3 * j + 1] = L > 1 ? sqrt(ss / (double)(L - 1)) : qnan;
-        out[3 * j + 2] = sum;
-    }
 }
 
 #include "kura_capi.inc"

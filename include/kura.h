@@ -113,10 +113,14 @@ int kura_set_env_params(KuraHandle* h, int env0, int n,
 /* calc_psd_for_simple_eval (aDBS_RL/evaluate_HF_DBS.py:122-135) of n device
  * signals sig[j*ld ...] of len[j] float32 samples (an episode's concatenated
  * true LFP): band_pass_envelope filtfilt (butter(2, [12,30]/(fs/2))), |rfft/n|^2*2,
- * filtfilt(ones(12), 5, .) smoothing, sum over beta_a < f < beta_b with
- * f = k/(len*psd_dt).  out[j] (device f64) is NaN when the band lies within
- * 48 bins of either spectrum end (too short a signal).  Float64 throughout;
- * agrees with NumPy/SciPy to ~1e-12 relative (not bitwise: FFT vs direct DFT). */
+ * filtfilt(ones(12), 5, .) smoothing of the whole half spectrum, sum over
+ * beta_a < f < beta_b with f = k/(len*psd_dt).  Any length and band: the
+ * spectrum is a Bluestein DFT (power-of-two FFTs of 2^m >= 2*len-1 points).
+ * out[j] (device f64) is NaN for len[j] < 72, where the reference raises
+ * (scipy filtfilt needs len/2+1 > padlen = 36).  Float64 throughout; agrees
+ * with NumPy/SciPy to ~1e-12 relative (not bitwise: different FFT).
+ * All metric calls on one handle share its scratch buffer: issue them on one
+ * stream (growing the buffer synchronises the device). */
 int kura_psd_bbpow(KuraHandle* h, const float* sig, const int32_t* len, int64_t ld, int n, double psd_dt,
                    double beta_a, double beta_b, double* out, void* stream);
 /* the same metric of every env's current-episode true LFP (requires
@@ -132,9 +136,9 @@ int kura_episode_bbpow(KuraHandle* h, const uint8_t* mask, double psd_dt, double
  * environment/utils.py:835-836, and log_main_metrics = mean, std(ddof=1),
  * sum, custom_callbacks.py:28-31) of n device signals sig[j*ld ...] of len[j]
  * float32 samples.  out[3j..3j+2] (device f64) = mean, std, sum; NaN for
- * len[j] outside [1, ld] (std NaN for len 1).  Float64 direct DFT (O(len^2),
- * evaluation-time only); SciPy's hilbert of float32 input runs in complex64,
- * so the reference agrees to ~1e-5 relative, the float64 restatement to ~1e-10. */
+ * len[j] outside [1, ld] (std NaN for len 1).  Float64 Bluestein DFTs
+ * (O(len log len)); SciPy's hilbert of float32 input runs in complex64, so
+ * the reference agrees to ~1e-5 relative, the float64 restatement to ~1e-10. */
 int kura_envelope_stats(KuraHandle* h, const float* sig, const int32_t* len, int64_t ld, int n, double* out,
                         void* stream);
 /* the same statistics of every env's current-episode true LFP (requires

@@ -3,7 +3,7 @@
 CPU: the restatement oracle/kura_eval.py against the reference function's own
 outputs (tests/golden/make_golden_eval.py).  GPU: kura_psd_bbpow and the
 per-env episode record (KuraVectorEnv(episode_metrics=True)) against the
-restatement; float64 with a direct DFT instead of pocketfft, so the bar is
+restatement; float64 Bluestein FFTs instead of pocketfft, so the bar is
 relative 1e-10, not bitwise."""
 import hashlib
 import importlib
@@ -44,8 +44,37 @@ def test_gpu_psd_bbpow_matches_reference():
     sig = signals()
     got = sim.psd_bbpow(sig, psd_dt=float(G["psd_dt"]))
     np.testing.assert_allclose(got, G["psd_bbpow"], rtol=RTOL, atol=0)
-    # too short for the band to clear the spectrum ends -> NaN, not a wrong value
-    assert np.isnan(sim.psd_bbpow([sig[0][:2000]])[0])
+    # any length scipy accepts (the smoothing filtfilt needs L/2 + 1 > 36): the
+    # whole spectrum is computed (Bluestein DFT), so short episodes get their
+    # value; shorter signals, where the reference raises, give NaN
+    short = [sig[0][:n] for n in (72, 73, 200, 2000, 2001)]
+    # (a 200-sample episode puts little power in the band: its value is bounded
+    # by the FFT rounding of the whole spectrum, ~1e-16 of the signal energy)
+    np.testing.assert_allclose(sim.psd_bbpow(short), kura_eval.calc_psd_for_simple_eval(short, 5e-4),
+                               rtol=RTOL, atol=1e-11)
+    with pytest.raises(ValueError):
+        kura_eval.calc_psd_for_simple_eval([sig[0][:71]], 5e-4)
+    assert np.isnan(sim.psd_bbpow([sig[0][:71]])[0])
+    sim.close()
+
+
+@pytest.mark.gpu
+def test_gpu_psd_long_episode_wide_band():
+    """Episodes far longer than a training episode (here 3 x 105k samples, the
+    callback's 12.5-33.5 Hz band = 3900 bins): no band-width limit."""
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    sim_mod = importlib.import_module("dbs-gym_amd.sim")
+    cfg = sim_mod.make_config(kura.reference_params("env0"), 4, reward_func="bbpow_action")
+    sim = sim_mod.KuraSim(cfg, 0)
+    base = signals()
+    long = [np.tile(base[0], 1 + 315_000 // len(base[0]))[:315_001 - k] for k in range(3)]
+    got = sim.psd_bbpow(long, beta=(12.5, 33.5))
+    want = kura_eval.calc_psd_for_simple_eval(long, 5e-4, 12.5, 33.5)
+    np.testing.assert_allclose(got, want, rtol=RTOL, atol=0)
+    env_got = sim.envelope_stats(long)
+    np.testing.assert_allclose(env_got, kura_eval.envelope_stats(long), rtol=ENV_RTOL, atol=0)
     sim.close()
 
 
@@ -82,7 +111,7 @@ from make_golden_envelope import edge_signals  # noqa: E402
 
 GE = np.load(os.path.join(ROOT, "tests", "golden", "reference_envelope_golden.npz"))
 ENV_REF_RTOL = 2e-5   # the reference's hilbert runs in complex64 (float32 input)
-ENV_RTOL = 1e-9       # GPU float64 direct DFT vs the float64 restatement (pocketfft)
+ENV_RTOL = 1e-9       # GPU float64 Bluestein FFT vs the float64 restatement (pocketfft)
 
 
 def _env_signals():
