@@ -41,6 +41,9 @@ def parse():
     ap.add_argument("--envs", type=int, default=4096, help="envs per GPU (weak scaling)")
     ap.add_argument("--global-envs", type=int, default=0,
                     help="total envs over all ranks (strong scaling: each rank owns global/world of them)")
+    ap.add_argument("--part-osc", type=int, default=-1,
+                    help="N > 1024: oscillators per workgroup of a split env group (256/512/1024; -1 = auto: "
+                         "the largest that gives every CU a workgroup)")
     ap.add_argument("--episode", action="store_true",
                     help="also run one whole episode through KuraVectorEnv (autoreset included) -> extra.episode")
     ap.add_argument("--episode-steps", type=int, default=0, help="episode length for --episode (0 = the config's)")
@@ -69,7 +72,9 @@ def build_shard(args, rank):
         plist.append(kura.fill_driver_arrays(p, w0_seed=10_000_000 + args.seed + gid))
     hosts, shared = kura.build_batch(plist)
     omega, g_stim, g_rec, theta0 = kura.reset_arrays(hosts)
-    cfg = sim_mod.make_config(base, B, reward_func=args.reward)
+    cfg = sim_mod.make_config(base, B, reward_func=args.reward,
+                              part_osc=(sim_mod.auto_part_osc(args.osc, B) if getattr(args, "part_osc", -1) < 0
+                                        else args.part_osc))
     bins = kura.spectral.beta_bins(cfg.window, base["verbose_dt"])
     ctab, stab = kura.spectral.twiddles(cfg.window, bins)
     return cfg, shared["alpha"].astype(np.float32), omega, g_stim, g_rec, theta0, ctab, stab, shared["gain"]
@@ -190,12 +195,15 @@ def cpu_baseline(args):
     return out
 
 
-def kernel_name(N):
-    """The step kernel instantiation libkura launches for N oscillators."""
-    return f"kura_step_kernel<{min(N, 1024) // 256}, {'true' if N > 1024 else 'false'}>"
+def kernel_name(N, part=0):
+    """The step kernel instantiation libkura launches for N oscillators (split
+    groups of `part` oscillators per workgroup when N > 1024)."""
+    if N > 1024:
+        return f"kura_step_kernel<{(part or 1024) // 256}, true>"
+    return f"kura_step_kernel<{N // 256}, false>"
 
 
-def pmc_traffic(N, B):
+def pmc_traffic(N, B, part=0):
     """Bytes per launch of the step kernel from the committed rocprofv3 PMC
     passes (tools/rocprof_run.sh + tools/summarize_rocprof.py: FETCH_SIZE x2 +
     WRITE_SIZE, the same bench command).  PMC counters cannot be read from
@@ -209,7 +217,7 @@ def pmc_traffic(N, B):
         wl = d["bench_under_trace"]["config"]["workload"]
         if f"N={N} " not in wl or f"x {B} envs" not in wl:
             return None, None, None
-        k = d["kernels"][kernel_name(N)]
+        k = d["kernels"][kernel_name(N, part)]
         return (k["traffic_bytes_per_dispatch"], f"profiles/latest_rocprof.json ({d['source']}): FETCH_SIZE*2 + WRITE_SIZE",
                 k.get("effective_clock_ghz"))
     except (OSError, KeyError, ValueError):
@@ -358,7 +366,7 @@ def main():
         # window r/w (f64 ring + f32 obs), outputs; alpha once per launch
         bytes_env = 8 * N + 4 * N + 8 * cfg.n_elec * N + 8 * max(cfg.n_rec, 0) * N + (8 + 8 + 4) * cfg.window + 64
         bytes_launch = B * bytes_env + 4 * N * N
-        traffic, traffic_src, clock_ghz = pmc_traffic(N, B)
+        traffic, traffic_src, clock_ghz = pmc_traffic(N, B, cfg.part_osc)
         out = {
             "metric": (f"env steps/sec (whole node), N={N} osc x {world * B} envs over {world} GPUs" if args.global_envs
                        else f"env steps/sec (whole node), N={N} osc x {B} envs per GPU"),
@@ -376,11 +384,12 @@ def main():
             "config": {"workload": f"{args.config} reference step(), N={N} oscillators x {B} envs per GPU, "
                                    f"adaptive Dopri5 rtol=atol=1e-5, W={cfg.window}, reward={args.reward}"
                                    + (", per-env K~U(0.3,0.8)" if args.random_k else ", K=0.52"),
-                       "global_envs": world * B, "parallelism": f"env-shard x{world} (no collectives)"},
+                       "global_envs": world * B, "parallelism": f"env-shard x{world} (no collectives)"}
+                      | ({"part_osc": cfg.part_osc or 1024} if N > 1024 else {}),
             "roofline": {"bound": "mfma", "achieved": achieved_tf, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
                          "frac": achieved_tf / PEAK_FP32_TFLOPS, "traffic": traffic,
                          "traffic_source": traffic_src,
-                         "kernel": kernel_name(N), "avg_kernel_ms": avg_kernel_s * 1e3,
+                         "kernel": kernel_name(N, cfg.part_osc), "avg_kernel_ms": avg_kernel_s * 1e3,
                          "flop_per_launch": flop_per_launch, "useful_rhs_per_launch": useful_rhs,
                          "hbm_alg_bytes_per_launch": bytes_launch,
                          "hbm_alg_gbs": bytes_launch / avg_kernel_s / 1e9},

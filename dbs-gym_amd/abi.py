@@ -68,7 +68,8 @@ class KuraConfig(ctypes.Structure):
         ("bins", c_int32 * KURA_MAX_BINS),
         ("padlen", c_int32),
         ("episode_cap", c_int32),
-        ("reserved_i", c_int32 * 3),
+        ("part_osc", c_int32),
+        ("reserved_i", c_int32 * 2),
         ("dt", c_double),
         ("width", c_double),
         ("pause", c_double),

@@ -92,11 +92,12 @@ struct DevParams {
     unsigned long long* stats;  // [KURA_NSTATS] (kura.h)
     unsigned long long* stamps; // [NWAVES][KURA_NSTAMP] phase cycle counters (KURA_STAMPS builds only)
     // split groups (N > 1024): npart workgroups share an env group, each owns
-    // 1024 oscillators; they exchange sin/cos images and partial sums through
+    // N/npart oscillators (a part: 256, 512 or 1024, KuraConfig.part_osc);
+    // they exchange sin/cos images and partial sums through
     // global memory with agent-scope release/acquire (group_barrier).
     int npart;              // workgroups per env group (1 when N <= 1024)
     int npairs;             // env groups x npart
-    float* xg;              // [group][2][npart][xs_floats(1024)] sin/cos images
+    float* xg;              // [group][2][npart][xl_img(part/256)] sin/cos images
     float* xred;            // [group][2][npart][RC][16] f32 partial sums
     double* xredd;          // [group][2][npart][RC][16] f64 partial sums
     unsigned* gcnt;         // [group][16] arrival counters, zeroed before every launch
@@ -140,12 +141,13 @@ __shared__ double s_smp_r[E_WG][KURA_S_MAX + 2];
 #define XS_HALF 132
 #define XS_BLOCK 264
 // split groups (N > 1024)
-#define XL_NL 1024                       // oscillators per part
-#define XL_IMG (XL_NL / 8 * XS_BLOCK)    // floats of one part's LDS/global image
+#define XL_NL 1024                       // default (largest) oscillators per part
 #define XL_KC 512                        // oscillators per streamed GEMM chunk
 #define XL_CIMG (XL_KC / 8 * XS_BLOCK)   // floats of one chunk image
 #define XL_SPIN_MAX (1u << 25)
 __host__ __device__ constexpr int xs_floats(int N) { return (N / 8) * XS_BLOCK; }
+// floats of one part's LDS / global sin/cos image (TPW column tiles per wave)
+__host__ __device__ constexpr int xl_img(int tpw) { return xs_floats(tpw * 256); }
 __device__ __forceinline__ int xs_idx(int row, int k) {
     return (k >> 3) * XS_BLOCK + (k & 1) * XS_HALF + (row << 2) + ((k >> 1) & 3);
 }
@@ -283,7 +285,7 @@ __device__ __forceinline__ void lds_barrier() {
 // Split-group GEMM (N > 1024): the same MFMA chain over all N oscillators
 // (k ascending, so P/Q are bit-identical to coupling_gemm's), with the
 // 32 x N sin/cos operand streamed from the group's global image (xg) through
-// two LDS chunk buffers of XL_KC oscillators, and this workgroup's 1024 output
+// two LDS chunk buffers of XL_KC oscillators, and this workgroup's TPW*256 output
 // columns (col0 ..) of alpha.
 template <int TPW>
 __device__ __forceinline__ void coupling_gemm_xl(const float* __restrict__ xg, const float* __restrict__ alpha_sw,
@@ -765,9 +767,11 @@ __device__ __forceinline__ void group_sum(const DevParams& p, Part& pt, float (&
         }
 }
 
-// Publish this part's sin/cos image (LDS, XL_IMG floats) into the group's
+// Publish this part's sin/cos image (LDS, xl_img(TPW) floats) into the group's
 // image buffer and wait until every part has published its own.
+template <int TPW>
 __device__ __forceinline__ const float* group_publish_x(const DevParams& p, Part& pt, const float* Xs) {
+    constexpr int XL_IMG = xl_img(TPW);
     const int grp = __builtin_amdgcn_readfirstlane(pt.group), npart = __builtin_amdgcn_readfirstlane(pt.npart);
     const size_t img = ((size_t)grp * 2 + (__builtin_amdgcn_readfirstlane(pt.xs_n) & 1)) * npart * XL_IMG;
     float* dst = uniform_ptr(p.xg + img + (size_t)__builtin_amdgcn_readfirstlane(pt.part) * XL_IMG);
@@ -1188,8 +1192,8 @@ __device__ void solve_wg(const DevParams& __restrict__ p, float* Xs, int env_bas
         STAMP(1);
         const float* xown = nullptr;
         if constexpr (XL) {
-            const float* xgrp = uniform_ptr(group_publish_x(p, pt, Xs));   // all parts' images of this stage
-            xown = xgrp + (size_t)__builtin_amdgcn_readfirstlane(pt.part) * XL_IMG;
+            const float* xgrp = uniform_ptr(group_publish_x<TPW>(p, pt, Xs));   // all parts' images of this stage
+            xown = xgrp + (size_t)__builtin_amdgcn_readfirstlane(pt.part) * xl_img(TPW);
             coupling_gemm_xl<TPW>(xgrp, p.alpha_sw, Xs, NG, col0, acc);
         } else {
             coupling_gemm<TPW>(Xs, p.alpha_sw, acc);
@@ -1431,7 +1435,7 @@ __device__ __forceinline__ Part make_part(const DevParams& p, int pair) {
     pt.group = pair / p.npart;
     pt.part = pair - pt.group * p.npart;
     pt.ng = p.N;
-    pt.col0 = pt.part * XL_NL;
+    pt.col0 = pt.part * (p.N / p.npart);
     pt.pair = pair;
     pt.ep = 0;
     pt.xs_n = 0;
@@ -1550,7 +1554,7 @@ __device__ __forceinline__ void step_pair(const DevParams& p, Part& pt, float* X
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, tid = threadIdx.x;
     const int N = p.N;
     const int env_base = pt.group * E_WG;
-    const int c0 = XL ? pt.col0 : 0, c1 = XL ? pt.col0 + XL_NL : N;   // oscillators of this workgroup
+    const int c0 = XL ? pt.col0 : 0, c1 = XL ? pt.col0 + TPW * 256 : N;   // oscillators of this workgroup
     __syncthreads();  // previous pair's LDS readers
     if (!XL && p.desync_cycles > 0 && (blockIdx.x & 1)) {
         // every workgroup runs the same phase sequence, so without an offset
@@ -1697,6 +1701,20 @@ __device__ __forceinline__ void step_pair(const DevParams& p, Part& pt, float* X
     if (!XL || pt.part == 0) flush_stats(p, rhs, env_base);
 }
 
+// Split groups call the step body out of line.  Inlined into the persistent
+// pair loop, the TPW = 1 split instantiation (parts of 256) came out of
+// ROCm 7.2's compiler with one env slot of every lane (q = 4) integrated
+// wrongly -- deterministic, gone at -O3 with this call boundary, present at
+// -O2 as well (tools/parity_probe.py, profiles/r02_part256_probe.txt); the
+// GPU parity suite covers every instantiation.
+template <int TPW, bool XL>
+__device__ __noinline__ void step_pair_call(const DevParams& p, Part& pt, float* Xs, const float* __restrict__ action,
+                                            float* __restrict__ obs, double* __restrict__ reward,
+                                            uint8_t* __restrict__ done, float* __restrict__ lfp_true,
+                                            double* __restrict__ lfp_rec, int* __restrict__ nsamp) {
+    step_pair<TPW, XL>(p, pt, Xs, action, obs, reward, done, lfp_true, lfp_rec, nsamp);
+}
+
 template <int TPW, bool XL>
 __global__ __launch_bounds__(NTHREADS) void kura_step_kernel(DevParams p, const float* __restrict__ action,
                                                              float* __restrict__ obs, double* __restrict__ reward,
@@ -1707,7 +1725,7 @@ __global__ __launch_bounds__(NTHREADS) void kura_step_kernel(DevParams p, const 
 #pragma unroll 1
         for (int pair = blockIdx.x; pair < p.npairs; pair += gridDim.x) {
             Part pt = make_part(p, pair);
-            step_pair<TPW, XL>(p, pt, Xs, action, obs, reward, done, lfp_true, lfp_rec, nsamp);
+            step_pair_call<TPW, XL>(p, pt, Xs, action, obs, reward, done, lfp_true, lfp_rec, nsamp);
         }
     } else {
         Part pt = make_part(p, blockIdx.x);
@@ -1722,7 +1740,7 @@ __device__ __forceinline__ void reset_pair(const DevParams& p, Part& pt, float* 
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, tid = threadIdx.x;
     const int N = p.N, W = p.W;
     const int env_base = pt.group * E_WG;
-    const int c0 = XL ? pt.col0 : 0, c1 = XL ? pt.col0 + XL_NL : N;
+    const int c0 = XL ? pt.col0 : 0, c1 = XL ? pt.col0 + TPW * 256 : N;
     __syncthreads();
     ctl_clear();
     if (tid < E_WG) {

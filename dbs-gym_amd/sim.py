@@ -18,9 +18,25 @@ from . import spectral
 from .abi import KURA_S_MAX, KuraConfig, KuraSolverError, check, ptr
 
 
+def auto_part_osc(n_osc: int, n_envs: int, n_cu: int = 256) -> int:
+    """Split-group part width (N > 1024) for a handle of n_envs envs: the
+    largest of 1024 / 512 / 256 oscillators per workgroup that still gives
+    every compute unit of the GPU (MI355X: 256) a workgroup, 256 otherwise;
+    0 (not split) for N <= 1024."""
+    if n_osc <= 1024:
+        return 0
+    groups = -(-n_envs // 16)
+    for part in (1024, 512, 256):
+        if n_osc % part == 0 and groups * (n_osc // part) >= n_cu:
+            return part
+    return 256 if n_osc % 256 == 0 else 1024
+
+
 def make_config(params: dict, n_envs: int, reward_func: str | None = None, max_steps: int = 4096,
-                episode_cap: int = 0) -> KuraConfig:
-    """Build the C config from a reference params dict (env.py:277-338)."""
+                episode_cap: int = 0, part_osc: int = 0) -> KuraConfig:
+    """Build the C config from a reference params dict (env.py:277-338).
+    part_osc: split-group part width for N > 1024 (0 = 1024; auto_part_osc
+    picks one that fills the GPU)."""
     p = params
     step_len = p["electrode_width"] + p["electrode_pause"]                      # env.py:294
     wind_len = step_len * p["observe_wind_counts"]                               # env.py:296
@@ -68,6 +84,7 @@ def make_config(params: dict, n_envs: int, reward_func: str | None = None, max_s
     c.kn = np.float32(p["K"] / p["num_oscillators"])                            # env.py:264
     c.dt0 = np.float32(0.05)                                                     # env.py:267
     c.episode_cap = int(episode_cap)
+    c.part_osc = int(part_osc)
     return c
 
 

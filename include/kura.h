@@ -79,7 +79,11 @@ typedef struct KuraConfig {
     int32_t padlen;        /* filtfilt padlen for R2 (3*max(len(a),len(b)) = 15) */
     int32_t episode_cap;   /* >0: keep each env's true-LFP samples of the running episode (up to this
                               many) for kura_episode_bbpow (evaluate_HF_DBS.py:83,122-135); 0: off */
-    int32_t reserved_i[3];
+    int32_t part_osc;      /* N > 1024 (split env groups): oscillators per workgroup, 256, 512 or 1024
+                              (0 = 1024); smaller parts put more workgroups on the chip when the
+                              handle has few envs.  It fixes the solver's reduction order (the
+                              oracle follows it), so results depend on it bit for bit. */
+    int32_t reserved_i[2];
     double dt;             /* verbose_dt: save-grid spacing (units) */
     double width;          /* electrode_width: stimulation ON interval */
     double pause;          /* electrode_pause: OFF interval */

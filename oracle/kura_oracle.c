@@ -142,22 +142,26 @@ static double rm_part_f64(const double* x, int n) {
     return tot;
 }
 
-/* N > 1024: the kernel splits the oscillators into parts of 1024 (one
- * workgroup each); each part reduces in the order above and the part totals
- * are added in part order from +0. */
-float oracle_rm_f32(const float* x, int n) {
+/* N > 1024: the kernel splits the oscillators into parts of `part` (256,
+ * 512 or 1024; KuraConfig.part_osc, default 1024), one workgroup each; each
+ * part reduces in the order above (TPW = part/256) and the part totals are
+ * added in part order from +0. */
+static float rm_f32_parts(const float* x, int n, int part) {
     if (n <= 1024) return rm_part_f32(x, n);
     float tot = 0.0f;
-    for (int q = 0; q < n / 1024; ++q) tot = tot + rm_part_f32(x + (size_t)q * 1024, 1024);
+    for (int q = 0; q < n / part; ++q) tot = tot + rm_part_f32(x + (size_t)q * part, part);
     return tot;
 }
 
-double oracle_rm_f64(const double* x, int n) {
+static double rm_f64_parts(const double* x, int n, int part) {
     if (n <= 1024) return rm_part_f64(x, n);
     double tot = 0.0;
-    for (int q = 0; q < n / 1024; ++q) tot = tot + rm_part_f64(x + (size_t)q * 1024, 1024);
+    for (int q = 0; q < n / part; ++q) tot = tot + rm_part_f64(x + (size_t)q * part, part);
     return tot;
 }
+
+float oracle_rm_f32(const float* x, int n) { return rm_f32_parts(x, n, 1024); }
+double oracle_rm_f64(const double* x, int n) { return rm_f64_parts(x, n, 1024); }
 
 static double r64_dot_f64(const double* x, const double* w, int n) {
     double p[64];
@@ -206,6 +210,7 @@ typedef struct {
     float* alphaT; /* alphaT[j*N + i] = alpha[i][j] */
     float* kn_env; /* per-env float32(K/N) (oracle_set_gain), NULL -> cfg.kn */
     int kn_n;
+    int part;      /* split-group part width (N > 1024): cfg.part_osc or 1024 */
 } OCtx;
 
 static float kn_of(const OCtx* o, int b) { return (o->kn_env && b < o->kn_n) ? o->kn_env[b] : o->cfg.kn; }
@@ -215,6 +220,7 @@ void* oracle_create(const KuraConfig* cfg, const float* alpha) {
     if (!o) return NULL;
     o->cfg = *cfg;
     o->N = cfg->n_osc;
+    o->part = cfg->part_osc > 0 ? cfg->part_osc : 1024;
     int N = o->N;
     o->alphaT = (float*)malloc(sizeof(float) * (size_t)N * N);
     if (!o->alphaT) { free(o); return NULL; }
@@ -320,7 +326,7 @@ static void rhs(const OCtx* o, Work* w, const float* y, const float* omega, cons
 static void lfp_row(const OCtx* o, Work* w, const float* row, const double* g_rec, float* naive, double* rec) {
     const int N = o->N;
     for (int j = 0; j < N; ++j) w->cosrow[j] = kdm_cosf(row[j]);
-    float m = oracle_rm_f32(w->cosrow, N) / (float)N;
+    float m = rm_f32_parts(w->cosrow, N, o->part) / (float)N;
     *naive = m;
     if (o->cfg.rec_kernel == KURA_REC_GAUSSIAN) {
         /* sum_r mean(cos * g_r) evaluated as mean(cos * G), G = g_0 + g_1 + ...
@@ -332,7 +338,7 @@ static void lfp_row(const OCtx* o, Work* w, const float* row, const double* g_re
             for (int r = 1; r < o->cfg.n_rec; ++r) G = G + g_rec[(size_t)r * N + j];
             w->prod[j] = (double)w->cosrow[j] * G;
         }
-        *rec = 0.0 + oracle_rm_f64(w->prod, N) / (double)N;
+        *rec = 0.0 + rm_f64_parts(w->prod, N, o->part) / (double)N;
     } else {
         *rec = (double)m;
     }
@@ -421,7 +427,7 @@ static void solve(const OCtx* o, Work* w, const Grid* g, float* y_start, const f
             float q = e / den;
             w->cosrow[i] = q * q; /* scratch */
         }
-        float mean = oracle_rm_f32(w->cosrow, N) / (float)N;
+        float mean = rm_f32_parts(w->cosrow, N, o->part) / (float)N;
         /* non-finite state or RHS reaches the error norm: the solve fails
          * (KURA_F_NONFINITE; the kernel's post_step makes the same test) */
         if (!(mean <= 3.40282346638528859812e+38f)) { st->flags |= KURA_F_NONFINITE; break; }

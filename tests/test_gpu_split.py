@@ -1,7 +1,8 @@
 """Split env groups (N > 1024): one env group of 16 spread over N/1024
 workgroups that exchange sin/cos images and partial sums through global
 memory.  GPU results must stay bit-identical to the oracle (whose RM order
-adds the 1024-oscillator part totals in part order)."""
+adds the part totals in part order; parts of 1024 by default, 512 or 256
+oscillators with KuraConfig.part_osc)."""
 import importlib
 import os
 
@@ -21,9 +22,10 @@ def torch_gpu():
     return torch
 
 
-def _pair(torch, N, B, steps, reward="bbpow_action", name="env0", gains=None):
+def _pair(torch, N, B, steps, reward="bbpow_action", name="env0", gains=None, part=0):
     sim_mod = importlib.import_module("dbs-gym_amd.sim")
     cfg, alpha, omega, gs, gr, th0, ct, st, _ = make_case(name, N, B, reward=reward)
+    cfg.part_osc = part
     sim = sim_mod.KuraSim(cfg, 0)
     sim.set_coupling(alpha)
     sim.set_env_params(omega, gs, gr)
@@ -71,3 +73,16 @@ def test_split_persistent_pair_loop(torch_gpu, monkeypatch):
 def test_split_n8192_stress_config(torch_gpu):
     """BASELINE.json configs[4]: N=8192 all-to-all coupling (8 parts per group)."""
     _pair(torch_gpu, 8192, 16, 2)
+
+
+@pytest.mark.parametrize("part,name,reward", [(256, "env0", "bbpow_action"), (512, "env1", "temp_const_action")])
+def test_split_small_parts(torch_gpu, part, name, reward):
+    """Parts of 256 / 512 oscillators (TPW = 1 / 2 split instantiations): the
+    strong-scaling stress form, where few envs per GPU must still fill the CUs."""
+    _pair(torch_gpu, 2048, 19, 3, reward=reward, name=name, part=part)
+
+
+def test_split_n8192_parts256(torch_gpu):
+    """N=8192 with parts of 256: 32 workgroups per env group (with 128 envs per
+    GPU, BASELINE configs[4] over 8 GPUs, 8 groups fill the 256 CUs)."""
+    _pair(torch_gpu, 8192, 16, 1, part=256)

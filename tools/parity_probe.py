@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Diagnostic: run GPU vs oracle for a few steps and report the first
-difference (step, output, env, index).  Usage: parity_probe.py ENV N B STEPS ACT"""
+difference (step, output, env, index).
+Usage: [PART=256] parity_probe.py ENV N B STEPS ACT [LIB|-]"""
 import importlib
 import os
 import sys
@@ -18,7 +19,9 @@ def main():
     import torch
     sim_mod = importlib.import_module("dbs-gym_amd.sim")
     cfg, alpha, omega, gs, gr, th0, ct, st, _ = make_case(name, N, B)
-    sim = sim_mod.KuraSim(cfg, 0, lib_path=sys.argv[6] if len(sys.argv) > 6 else None)
+    cfg.part_osc = int(os.environ.get("PART", "0"))
+    lib = sys.argv[6] if len(sys.argv) > 6 and sys.argv[6] != "-" else None
+    sim = sim_mod.KuraSim(cfg, 0, lib_path=lib)
     sim.set_coupling(alpha)
     sim.set_env_params(omega, gs, gr)
     sim.set_spectral(ct, st)
