@@ -14,9 +14,12 @@ __version__ = "0.1.0"
 
 def __getattr__(name):
     # torch-dependent pieces are imported lazily so host-only helpers stay cheap
-    if name in ("KuraSim", "make_config"):
+    if name in ("KuraSim", "make_config", "auto_part_osc"):
         from . import sim
         return getattr(sim, name)
+    if name == "KuraSB3VecEnv":
+        from . import sb3
+        return sb3.KuraSB3VecEnv
     if name in ("KuraVectorEnv", "SpatialKuramoto"):
         from . import vec_env
         return getattr(vec_env, name)
