@@ -1,8 +1,10 @@
+# GPU vs oracle first-difference probe over a few configurations (via gpurun):
+#   bash tools/probe_parts.sh "PART ENV N B STEPS ACT" ...   (PART 0 = default)
 set -e
-O=gpurun_out/probe_swap2; mkdir -p $O; : > $O/p.txt
-for lib in libkura_v1.so; do
-for cfg in "env0 1024 16 2 rand"; do
-  echo "== $lib $cfg" >> $O/p.txt
-  timeout -k 10 120 python3 -u tools/parity_probe.py $cfg $PWD/dbs-gym_amd/csrc/$lib >> $O/p.txt 2>&1
-done; done
+O=gpurun_out/probe; mkdir -p $O; : > $O/p.txt
+for cfg in "$@"; do
+  set -- $cfg
+  echo "== part=$1 $2 N=$3 B=$4 steps=$5 act=$6" >> $O/p.txt
+  PART=$1 timeout -k 10 120 python3 -u tools/parity_probe.py $2 $3 $4 $5 $6 >> $O/p.txt 2>&1
+done
 grep -v amdgpu.ids $O/p.txt
