@@ -1,0 +1,45 @@
+"""Host-side pieces of the strong-scaling / split-group configuration (no GPU):
+the automatic part width, the kernel naming the bench reports, and that the
+part width reaches the C config (and so the oracle's RM order)."""
+import importlib
+import sys
+
+import pytest
+
+from helpers import ROOT, kura
+
+sys.path.insert(0, ROOT)
+
+
+def test_auto_part_osc_fills_the_cus():
+    sim = importlib.import_module("dbs-gym_amd.sim")
+    assert sim.auto_part_osc(1024, 4096) == 0            # not split
+    assert sim.auto_part_osc(8192, 1024) == 1024         # 64 groups x 8 parts = 512 >= 256
+    assert sim.auto_part_osc(8192, 256) == 512           # 16 groups x 16 parts = 256
+    assert sim.auto_part_osc(8192, 128) == 256           # strong form at 8 GPUs: 8 x 32 = 256
+    assert sim.auto_part_osc(2048, 16) == 256            # too few envs for any width: smallest
+    for n, b in ((2048, 19), (4096, 300), (8192, 4096)):
+        part = sim.auto_part_osc(n, b)
+        assert part in (256, 512, 1024) and n % part == 0
+
+
+def test_part_width_reaches_the_config():
+    sim = importlib.import_module("dbs-gym_amd.sim")
+    p = kura.synthetic_params("env0", 2048)
+    assert sim.make_config(p, 32, reward_func="bbpow_action").part_osc == 0
+    assert sim.make_config(p, 32, reward_func="bbpow_action", part_osc=256).part_osc == 256
+
+
+def test_bench_kernel_name():
+    bench = importlib.import_module("bench")
+    assert bench.kernel_name(1024) == "kura_step_kernel<4, false>"
+    assert bench.kernel_name(512) == "kura_step_kernel<2, false>"
+    assert bench.kernel_name(8192) == "kura_step_kernel<4, true>"
+    assert bench.kernel_name(8192, 256) == "kura_step_kernel<1, true>"
+    assert bench.kernel_name(8192, 512) == "kura_step_kernel<2, true>"
+
+
+@pytest.mark.parametrize("flag", ["--episode", "--global-envs", "--part-osc", "--episode-metrics"])
+def test_bench_modes_are_documented(flag):
+    src = open(f"{ROOT}/bench.py").read()
+    assert f'"{flag}"' in src
