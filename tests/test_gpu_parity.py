@@ -142,3 +142,12 @@ def test_phase_gate_1000_steps(torch_gpu):
     rel = np.abs(g["y"].astype(np.float64) - o["y"]) / np.maximum(np.abs(o["y"].astype(np.float64)), 1e-30)
     assert rel.max() <= PHASE_RTOL
     np.testing.assert_array_equal(g["y"], o["y"])
+
+
+def test_phase_gate_1000_steps_env1_r2(torch_gpu):
+    """The same gate on env1 (recorder-weighted f64 LFP, per-env contacts) with
+    the R2 filter reward at N=1024 (TPW=4 gaussian save passes)."""
+    g, o = _run_pair(torch_gpu, "env1", 1024, 8, "temp_const_action", 1000, "rand", check_every=250)
+    rel = np.abs(g["y"].astype(np.float64) - o["y"]) / np.maximum(np.abs(o["y"].astype(np.float64)), 1e-30)
+    assert rel.max() <= PHASE_RTOL
+    np.testing.assert_array_equal(g["y"], o["y"])
