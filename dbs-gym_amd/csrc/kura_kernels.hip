@@ -113,7 +113,7 @@ struct DevParams {
 // Diagnostic phase timers (compile with -DKURA_STAMPS): per wave, cycles
 // spent in each phase (tools/phase_stamps.py names them), accumulated with
 // s_memtime and added into p.stamps[wave][KURA_NSTAMP] at the end.
-#define KURA_NSTAMP 16
+#define KURA_NSTAMP 20
 #ifdef KURA_STAMPS
 #define STAMP_DECL unsigned long long st_acc[KURA_NSTAMP] = {}; unsigned long long st_last = __builtin_amdgcn_s_memtime();
 #define STAMP(k) do { unsigned long long n_ = __builtin_amdgcn_s_memtime(); st_acc[k] += n_ - st_last; st_last = n_; } while (0)
@@ -551,11 +551,24 @@ __device__ __forceinline__ void stage_input(const Slot& ws, float* Xs, int s, co
         for (int j = 0; j < 6; ++j)
             if (j < nmem) load8(ws, SL_F0 + j, t, f[b][j]);
     };
+#ifdef KURA_STAMPS_SI
+    // diagnostic: no prefetch; per tile: record-load latency (16), arithmetic
+    // (17), LDS operand writes (18) -- the compiler moves arithmetic across the
+    // (17) boundary, so read 17 + 18 together
+#pragma unroll
+    for (int t = 0; t < TPW; ++t) {
+        const int b = 0;
+        STAMP(19);
+        fetch(t, 0);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        STAMP(16);
+#else
     fetch(0, 0);
 #pragma unroll
     for (int t = 0; t < TPW; ++t) {
         const int b = t & 1;
         if (t + 1 < TPW) fetch(t + 1, b ^ 1);
+#endif
         if (have_prev) {
 #pragma unroll
             for (int q = 0; q < 8; ++q) f[b][5][q] = fprev[t][q];  // f_{s-1}; slot 5 is unused when have_prev
@@ -585,6 +598,22 @@ __device__ __forceinline__ void stage_input(const Slot& ws, float* Xs, int s, co
 #pragma unroll
             for (int q = 0; q < 8; ++q) th[q] = kdm_fmod2pi(ys[q]);
         }
+#ifdef KURA_STAMPS_SI
+        float snv[8], csv[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) kdm_sincosf(th[q], &snv[q], &csv[q]);
+        asm volatile("" ::: "memory");
+        STAMP(17);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const int e = mfma_env(q, lane);
+            Xs[xs_idx(e, i)] = snv[q];
+            Xs[xs_idx(16 + e, i)] = csv[q];
+        }
+        if (s == 6) store8(ws, SL_Y1, t, ys);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        STAMP(18);
+#else
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
             float sn, cs;
@@ -594,6 +623,7 @@ __device__ __forceinline__ void stage_input(const Slot& ws, float* Xs, int s, co
             Xs[xs_idx(16 + e, i)] = cs;
         }
         if (s == 6) store8(ws, SL_Y1, t, ys);
+#endif
     }
 }
 

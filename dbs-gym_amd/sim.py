@@ -290,7 +290,7 @@ class KuraSim:
         return out
 
     def stamps(self) -> np.ndarray:
-        out = np.zeros((8, 16), np.uint64)
+        out = np.zeros((8, 20), np.uint64)   # [wave][KURA_NSTAMP]
         check(self.lib, self.lib.kura_get_stamps(self._h, out.ctypes.data), "kura_get_stamps")
         return out
 

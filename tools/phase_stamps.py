@@ -13,15 +13,16 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 import __graft_entry__ as ge  # noqa: E402
 
-LIB = os.path.join(ge.CSRC, "libkura_stamps.so")
+SI = os.environ.get("SI") == "1"  # stage-input sub-phases (KURA_STAMPS_SI build, no record prefetch)
+LIB = os.path.join(ge.CSRC, "libkura_stamps_si.so" if SI else "libkura_stamps.so")
 PHASES = ["stage_input", "barrier1", "gemm", "epilogue", "barrier2", "post_err", "flag_sync", "post_decide",
           "post_saves", "post_fsal", "post_time", "save_setup", "save_loadwait", "save_compute", "save_publish",
-          "save_totals"]
+          "save_totals", "si_load", "si_compute", "si_lds", "si_misc"]
 
 
 def main():
     if not os.path.exists(LIB) or os.path.getmtime(LIB) < os.path.getmtime(os.path.join(ge.CSRC, "kura_kernels.hip")):
-        subprocess.run([ge.HIPCC, *ge.HIP_FLAGS, "-DKURA_STAMPS", "-o", LIB,
+        subprocess.run([ge.HIPCC, *ge.HIP_FLAGS, "-DKURA_STAMPS", *(["-DKURA_STAMPS_SI"] if SI else []), "-o", LIB,
                         os.path.join(ge.CSRC, "kura_kernels.hip")], check=True)
     import numpy as np
     import torch
