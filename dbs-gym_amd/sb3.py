@@ -24,6 +24,7 @@ from __future__ import annotations
 import time
 
 import numpy as np
+import torch
 
 from .vec_env import KuraVectorEnv
 
@@ -31,7 +32,7 @@ _REWARD_METHODS = ("reward_bbpow_action", "reward_temp_const_lfp_betafilt_action
 
 
 class KuraSB3VecEnv:
-    def __init__(self, venv: KuraVectorEnv, monitor: bool = True):
+    def __init__(self, venv: KuraVectorEnv, monitor: bool = True, obs_buffers: int | None = 4):
         if not venv.autoreset:
             raise ValueError("KuraSB3VecEnv needs a KuraVectorEnv with autoreset=True (DummyVecEnv semantics)")
         self.venv = venv
@@ -44,6 +45,15 @@ class KuraSB3VecEnv:
         self._ep_rew = np.zeros(self.num_envs, np.float64)
         self._ep_len = np.zeros(self.num_envs, np.int64)
         self._t0 = np.full(self.num_envs, time.time())
+        self._pin = None   # pinned host staging for the per-step device -> host copies
+        # observations are returned in a ring of obs_buffers preallocated host
+        # arrays (an array stays valid for obs_buffers - 1 further steps --
+        # SB3's rollout collection and evaluate_policy copy or drop it after
+        # one); None returns a fresh array every step, DummyVecEnv's exact
+        # semantics, at ~2x the host cost per step (page faults of a new
+        # (B, 1, W) array, tools/sb3_bench.py)
+        self.obs_buffers = obs_buffers
+        self._ring, self._ring_i = None, 0
 
     # ---- VecEnv core ----------------------------------------------------------
     def reset(self):
@@ -62,11 +72,8 @@ class KuraSB3VecEnv:
             raise RuntimeError("step_wait() without step_async()")
         a, self._actions = self._actions, None
         obs, rew, term, trunc, info = self.venv.step(a)
-        rew64 = rew.cpu().numpy()
-        dones = (term | trunc).cpu().numpy().astype(bool)
-        trunc_h = trunc.cpu().numpy().astype(bool)
-        term_h = term.cpu().numpy().astype(bool)
-        obs_h = obs.cpu().numpy()
+        obs_h, rew64, term_h, trunc_h = self._to_host(obs, rew, term, trunc)
+        dones = term_h | trunc_h
         self._ep_rew += rew64
         self._ep_len += 1
         infos = [{} for _ in range(self.num_envs)]
@@ -96,6 +103,33 @@ class KuraSB3VecEnv:
     def step(self, actions):
         self.step_async(actions)
         return self.step_wait()
+
+    def _to_host(self, obs, rew, term, trunc):
+        """All four step outputs to the host in one synchronisation: async
+        copies into pinned staging buffers, then a fresh obs array per step
+        (DummyVecEnv returns copies) made by a multithreaded torch copy --
+        a pageable `.cpu()` of the (B, 1, W) float32 observation costs ~4x
+        more at B=4096 (tools/sb3_bench.py)."""
+        if self._pin is None or self._pin[0].shape != obs.shape:
+            self._pin = (torch.empty(obs.shape, dtype=obs.dtype, pin_memory=True),
+                         torch.empty(rew.shape, dtype=rew.dtype, pin_memory=True),
+                         torch.empty(term.shape, dtype=torch.bool, pin_memory=True),
+                         torch.empty(trunc.shape, dtype=torch.bool, pin_memory=True))
+        po, pr, pt, pu = self._pin
+        po.copy_(obs, non_blocking=True)
+        pr.copy_(rew, non_blocking=True)
+        pt.copy_(term, non_blocking=True)
+        pu.copy_(trunc, non_blocking=True)
+        torch.cuda.current_stream(obs.device).synchronize()
+        if self.obs_buffers:
+            if self._ring is None or self._ring[0].shape != po.shape:
+                self._ring = [torch.zeros(po.shape, dtype=po.dtype) for _ in range(max(2, self.obs_buffers))]
+            out = self._ring[self._ring_i]
+            self._ring_i = (self._ring_i + 1) % len(self._ring)
+            out.copy_(po)
+        else:
+            out = po.clone()
+        return out.numpy(), pr.numpy().copy(), pt.numpy().copy(), pu.numpy().copy()
 
     def close(self) -> None:
         self.venv.close()

@@ -152,3 +152,31 @@ def test_sb3_adapter_matches_oracle(model):
     r = env.env_method("reward_bbpow_action", x, [0.4], indices=[0, 2])
     assert len(r) == 2 and r[0] == r[1]
     env.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("obs_buffers", [4, None])
+def test_sb3_host_observations(obs_buffers):
+    """The host staging of step(): obs equal the device observation, a ring of
+    obs_buffers arrays keeps each returned array intact for obs_buffers - 1
+    further steps, and obs_buffers=None returns a fresh array every step."""
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    vec = importlib.import_module("dbs-gym_amd.vec_env")
+    sb3 = importlib.import_module("dbs-gym_amd.sb3")
+    p = kura.synthetic_params("env0", 256)
+    venv = vec.KuraVectorEnv(p, num_envs=5, reward_func="bbpow_action", w0_seed=3)
+    env = sb3.KuraSB3VecEnv(venv, obs_buffers=obs_buffers)
+    env.reset()
+    rng = np.random.default_rng(0)
+    kept = []
+    for k in range(3):
+        obs, rew, dones, infos = env.step(rng.uniform(-1, 1, (5, 1)).astype(np.float32))
+        np.testing.assert_array_equal(obs, venv.sim.obs.view(5, 1, -1).cpu().numpy())
+        assert obs.dtype == np.float32 and rew.dtype == np.float32 and dones.dtype == bool
+        kept.append((obs, obs.copy()))
+    for a, snapshot in kept:          # three steps < a ring of 4: nothing overwritten yet
+        np.testing.assert_array_equal(a, snapshot)
+    assert len({id(a) for a, _ in kept}) == 3 and not np.shares_memory(kept[0][0], kept[1][0])
+    env.close()
