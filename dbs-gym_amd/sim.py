@@ -84,6 +84,8 @@ def make_config(params: dict, n_envs: int, reward_func: str | None = None, max_s
     c.kn = np.float32(p["K"] / p["num_oscillators"])                            # env.py:264
     c.dt0 = np.float32(0.05)                                                     # env.py:267
     c.episode_cap = int(episode_cap)
+    if part_osc and (part_osc not in (256, 512, 1024) or c.n_osc % part_osc):
+        raise ValueError(f"part_osc={part_osc}: expected 256, 512 or 1024 dividing num_oscillators={c.n_osc}")
     c.part_osc = int(part_osc)
     return c
 

@@ -28,6 +28,9 @@ def test_part_width_reaches_the_config():
     p = kura.synthetic_params("env0", 2048)
     assert sim.make_config(p, 32, reward_func="bbpow_action").part_osc == 0
     assert sim.make_config(p, 32, reward_func="bbpow_action", part_osc=256).part_osc == 256
+    for bad in (128, 768, 2048):
+        with pytest.raises(ValueError):
+            sim.make_config(p, 32, reward_func="bbpow_action", part_osc=bad)
 
 
 def test_bench_kernel_name():
