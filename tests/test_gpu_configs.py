@@ -98,3 +98,25 @@ def test_full_grid_b4096_sampled(torch_gpu, name, reward):
             np.testing.assert_array_equal(getattr(sim, key).cpu().numpy()[idx], ref[key], err_msg=f"{key} step {k}")
         _cmp_state({kk: v[idx] for kk, v in sim.get_state().items()}, o.state(), f"step {k}")
     sim.close()
+
+
+@pytest.mark.parametrize("name,N,elec,rec", [
+    ("env1", 512, [[4, 3, 4], [2, 5, 3], [6, 2, 5]], [[1, 1, 1], [6, 6, 2]]),   # 3 contacts, 2 recorders
+    ("env0", 1024, [[4, 3, 4], [3, 6, 2]], [[1, 1, 1]]),                        # 2 contacts, naive LFP
+    ("env1", 1024, [[4, 3, 4], [2, 5, 3], [6, 2, 5], [5, 5, 5]],
+     [[1, 1, 1], [6, 6, 2], [2, 6, 6], [5, 1, 3]]),                            # the 4 / 4 maximum
+])
+def test_multi_contact_parity(torch_gpu, name, N, elec, rec):
+    """Several stimulating contacts (pulse = sum_e g_e u_e, env.py:419-424, one
+    action per contact) and several recorders (sum over recorders of the
+    weighted LFP, env.py:404-412), up to the ABI's 4 / 4."""
+    g, o = _run_pair(torch_gpu, name, N, 19, "bbpow_action", 6, "rand", elec_coords=elec, rec_coords=rec,
+                     electrode_amps=[1.0] * len(elec))
+    np.testing.assert_array_equal(g["y"], o["y"])
+
+
+def test_largest_window_parity(torch_gpu):
+    """observe_wind_counts=142: W = 2556 samples, next to the kernel's 2560
+    limit (WPL_MAX = 40 samples per lane), R1 and the window ring at its largest."""
+    g, o = _run_pair(torch_gpu, "env0", 256, 19, "bbpow_action", 6, "rand", observe_wind_counts=142)
+    np.testing.assert_array_equal(g["ring"], o["ring"])
