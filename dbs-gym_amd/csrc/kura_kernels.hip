@@ -489,7 +489,7 @@ __device__ __forceinline__ void store8(const Slot& w, int slot, int t, const flo
 template <int TPW, bool XL>
 __device__ __forceinline__ void coupling_epilogue(const DevParams& __restrict__ p, const Slot& ws, const float* __restrict__ Xs,
                                                   const float* __restrict__ xown, const floatx16 (&acc)[TPW],
-                                                  int stage, bool pulse_on, float (&fout)[TPW][8]) {
+                                                  int stage, bool pulse_on) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     float w[TPW][8], u[TPW][8];
 #pragma unroll
@@ -524,7 +524,6 @@ __device__ __forceinline__ void coupling_epilogue(const DevParams& __restrict__ 
             const float tq = sn * Q;
             const float coup = __builtin_fmaf(cs, P, -tq);
             f[q] = __builtin_fmaf(knq[q], coup, w[t][q]) + u[t][q];
-            fout[t][q] = f[q];
         }
         store8(ws, SL_F0 + stage, t, f);
     }
@@ -533,17 +532,18 @@ __device__ __forceinline__ void coupling_epilogue(const DevParams& __restrict__ 
 // Stage input ys = y0 + chain_j(A[s][j] * h*f_j) (zero coefficients skipped,
 // as in the oracle), theta = fmod(ys, 2pi), sin/cos into the LDS operand.
 // Stage 0 is the solve's initial RHS at y0.  Tiles are software-pipelined:
-// the records of tile t+1 are requested before tile t is computed, and the
-// newest f (f_{s-1}, still in registers from the epilogue) is not reloaded
-// when have_prev.
+// the records of tile t+1 are requested before tile t is computed.  Every
+// f_j comes from its record, the newest (f_{s-1}) included: handing it over
+// in registers from the epilogue (round 1) only made the compiler spill it
+// across the stage barrier -- 32 dwords per lane per sweep to scratch and
+// back -- and cost 4 % of the step.
 template <int TPW>
-__device__ __forceinline__ void stage_input(const Slot& ws, float* Xs, int s, const float (&fprev)[TPW][8],
-                                            bool have_prev STAMP_PARAMS) {
+__device__ __forceinline__ void stage_input(const Slot& ws, float* Xs, int s STAMP_PARAMS) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     float h[8];
 #pragma unroll
     for (int q = 0; q < 8; ++q) h[q] = s_ctl[mfma_env(q, lane)].h;
-    const int nmem = have_prev ? s - 1 : s;  // f_0 .. f_{nmem-1} come from the records
+    const int nmem = s;  // f_0 .. f_{s-1}
     float y0[2][8], f[2][6][8];
     auto fetch = [&](int t, int b) __attribute__((always_inline)) {
         load8(ws, SL_Y0, t, y0[b]);
@@ -569,10 +569,6 @@ __device__ __forceinline__ void stage_input(const Slot& ws, float* Xs, int s, co
         const int b = t & 1;
         if (t + 1 < TPW) fetch(t + 1, b ^ 1);
 #endif
-        if (have_prev) {
-#pragma unroll
-            for (int q = 0; q < 8; ++q) f[b][5][q] = fprev[t][q];  // f_{s-1}; slot 5 is unused when have_prev
-        }
         const int i = 32 * (wave * TPW + t) + (lane & 31);
         float ys[8], th[8];
         int slow = 0;
@@ -580,8 +576,7 @@ __device__ __forceinline__ void stage_input(const Slot& ws, float* Xs, int s, co
         for (int q = 0; q < 8; ++q) {
             float v = y0[b][q];
             if (s > 0) {
-                // term j: f_j from the records, or (j == s-1, have_prev) from the epilogue
-#define KURA_FJ(j) ((have_prev && (j) == s - 1) ? f[b][5][q] : f[b][j][q])
+#define KURA_FJ(j) (f[b][j][q])
                 float acc = cA[s][0] * (h[q] * KURA_FJ(0));
                 if (s > 1 && cA[s][1] != 0.0f) acc = __builtin_fmaf(cA[s][1], h[q] * KURA_FJ(1), acc);
                 if (s > 2) acc = __builtin_fmaf(cA[s][2], h[q] * KURA_FJ(2), acc);
@@ -1213,8 +1208,7 @@ __device__ void solve_wg(const DevParams& __restrict__ p, float* Xs, int env_bas
     STAMP_DECL
     long long nrhs = 0;
     int s = 0;  // stage 0 = initial RHS at y0 (FSAL seed)
-    float fcur[TPW][8];
-    stage_input<TPW>(ws, Xs, 0, fcur, false STAMP_ARGS);
+    stage_input<TPW>(ws, Xs, 0 STAMP_ARGS);
     STAMP(0);
     for (;;) {
         floatx16 acc[TPW];
@@ -1229,14 +1223,14 @@ __device__ void solve_wg(const DevParams& __restrict__ p, float* Xs, int env_bas
             coupling_gemm<TPW>(Xs, p.alpha_sw, acc);
         }
         STAMP(2);
-        coupling_epilogue<TPW, XL>(p, ws, Xs, xown, acc, s, pulse_on, fcur);
+        coupling_epilogue<TPW, XL>(p, ws, Xs, xown, acc, s, pulse_on);
         STAMP(3);
         lds_barrier();  // every wave is done reading the operand before it is rewritten
         STAMP(4);
         ++nrhs;
         if (s > 0 && s < 6) {
             ++s;
-            stage_input<TPW>(ws, Xs, s, fcur, true STAMP_ARGS);   // f_{s-1} straight from the epilogue
+            stage_input<TPW>(ws, Xs, s STAMP_ARGS);
             STAMP(0);
             continue;
         }
@@ -1254,11 +1248,10 @@ __device__ void solve_wg(const DevParams& __restrict__ p, float* Xs, int env_bas
         lds_barrier();
         STAMP(6);
         if (s_any == 0) break;
-        // stage 1 of the next Dopri step: after stage 0 f_0 is still in
-        // registers; after a step f_0 is the FSAL select of post_step (records)
-        const bool prev = s == 0;
+        // stage 1 of the next Dopri step (f_0: the stage-0 record, or the
+        // FSAL select of post_step)
         s = 1;
-        stage_input<TPW>(ws, Xs, 1, fcur, prev STAMP_ARGS);
+        stage_input<TPW>(ws, Xs, 1 STAMP_ARGS);
         STAMP(0);
     }
     STAMP_FLUSH(p);
