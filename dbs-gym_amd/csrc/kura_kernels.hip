@@ -878,26 +878,14 @@ __device__ __forceinline__ void save_pass(const DevParams& __restrict__ p, const
     int fin = 0;  // wave-uniform: rounds holding some env's final row (bit k)
 #pragma unroll
     for (int k = 0; k < RCX; ++k) fin |= __any((flor >> (3 * k)) & 4) ? (1 << k) : 0;
-    // Final-state and captured-row stores go through wave-uniform buffer
-    // descriptors over this workgroup's 16 envs: one lane offset (VGPR) plus an
-    // (env slot, tile) offset in an SGPR.  Per-(q, t) 64-bit addresses were
-    // hoisted out of the tile loop and spilled (the largest block of the
-    // solver's scratch traffic), and the one build that miscomputed envs 8-15
-    // did so exactly in this final-state store.
-    constexpr int SROWS = KURA_S_MAX + 1;
-    const int env_lim = Bn - env_base;  // env slots >= this are padding
-    const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)uniform_ptr(p.y + (size_t)env_base * NG), 0, E_WG * NG * 4, 0x00020000);
-    const int yvoff = (4 * (lane >> 5) * NG + (lane & 31)) * 4;
-    int rvoff[8];  // captured rows: lane offset of round 0 of this pass (sol_state_ row si - lfp_from + pos0)
-    __amdgpu_buffer_rsrc_t rrs = yrs;
+    float* const yout = p.y;
+    float* const rows = p.rows;
+    int rbase[8];  // captured row index of round 0 of this pass: sol_state_ row si - lfp_from + pos0
     if (capture) {
-        rrs = __builtin_amdgcn_make_buffer_rsrc((void*)uniform_ptr(p.rows + (size_t)env_base * SROWS * NG), 0,
-                                                E_WG * SROWS * NG * 4, 0x00020000);
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
             const CtlE& c = s_ctl[mfma_env(q, lane)];
-            rvoff[q] = ((4 * (lane >> 5) * SROWS + c.si + r0 - c.lfp_from + c.pos0) * NG + (lane & 31)) * 4;
+            rbase[q] = c.si + r0 - c.lfp_from + c.pos0;
         }
     }
     // (2) dense output + LFP partials: every (round, env) of a tile is
@@ -946,24 +934,19 @@ __device__ __forceinline__ void save_pass(const DevParams& __restrict__ p, const
                 pn[k][q] = (f & 2) ? pn[k][q] + cr : pn[k][q];
                 if (gauss) pg[k][q] = (f & 2) ? pg[k][q] + (double)cr * G[q] : pg[k][q];
             }
-            const int tcol = col0 + 32 * (wave * TPW + t);  // wave-uniform
             if ((fin >> k) & 1) {  // the solve's last row: the new state
 #pragma unroll
                 for (int q = 0; q < 8; ++q) {
-                    const int eq = (q & 3) + 8 * (q >> 2);  // env slot of q in lane half 0
-                    if (((fl[q] >> (3 * k)) & 4) && mfma_env(q, lane) < env_lim)
-                        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[q]), yrs, yvoff,
-                                                              __builtin_amdgcn_readfirstlane((eq * NG + tcol) * 4), 0);
+                    const int env = env_base + mfma_env(q, lane);
+                    if (((fl[q] >> (3 * k)) & 4) && env < Bn) yout[(size_t)env * NG + col0 + i] = v[q];
                 }
             }
             if (capture) {
 #pragma unroll
                 for (int q = 0; q < 8; ++q) {
-                    const int eq = (q & 3) + 8 * (q >> 2);
-                    if (((fl[q] >> (3 * k)) & 1) && mfma_env(q, lane) < env_lim)
-                        __builtin_amdgcn_raw_buffer_store_b32(
-                            __float_as_uint(v[q]), rrs, rvoff[q] + k * NG * 4,
-                            __builtin_amdgcn_readfirstlane((eq * SROWS * NG + tcol) * 4), 0);
+                    const int env = env_base + mfma_env(q, lane);
+                    if (((fl[q] >> (3 * k)) & 1) && env < Bn)
+                        rows[((size_t)env * (KURA_S_MAX + 1) + rbase[q] + k) * NG + col0 + i] = v[q];
                 }
             }
         }
