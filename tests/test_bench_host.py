@@ -46,3 +46,18 @@ def test_bench_kernel_name():
 def test_bench_modes_are_documented(flag):
     src = open(f"{ROOT}/bench.py").read()
     assert f'"{flag}"' in src
+
+
+def test_rocprof_summary_backs_the_bench_roofline():
+    """The bench line's roofline.traffic comes from the committed rocprofv3
+    summary of the same workload, and that summary's traced kernel average
+    agrees with the HIP-event average measured in the traced run."""
+    import json
+    bench = importlib.import_module("bench")
+    d = json.load(open(f"{ROOT}/profiles/latest_rocprof.json"))
+    k = d["kernels"][bench.kernel_name(1024)]
+    traffic, src, clock = bench.pmc_traffic(1024, 4096)
+    assert traffic == k["traffic_bytes_per_dispatch"] > 0
+    assert d["source"] in src and 1.5 < clock < 2.6
+    hip_ms = d["bench_under_trace"]["avg_kernel_ms_hip_events"]
+    assert k["min_ms"] <= hip_ms and abs(k["avg_ms"] - hip_ms) / hip_ms < 0.05
