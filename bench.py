@@ -54,6 +54,10 @@ def parse():
                     help="bounded CPU-baseline budget in seconds (0 = skip), split over its legs")
     ap.add_argument("--seed", type=int, default=2024)
     ap.add_argument("--random-k", action="store_true", help="per-env K ~ U(0.3, 0.8) (north_star 'random K')")
+    # rehearsal of the N>1 path on a one-GPU box: every rank on cuda:0, gloo for the
+    # barrier / max-over-ranks (RCCL cannot put two ranks on one device)
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"])
+    ap.add_argument("--share-device", action="store_true", help="every rank uses cuda:0 (rehearsal only)")
     return ap.parse_args()
 
 
@@ -266,7 +270,7 @@ def episode_bench(args, rank, world, local_rank):
         dist.barrier()
     el = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        t = torch.tensor([el], dtype=torch.float64, device=dev if args.dist_backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
     bt = env.boundary_times[-1] if env.boundary_times else {}
@@ -285,7 +289,7 @@ def main():
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    local_rank = 0 if args.share_device else int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus and rank == 0:
         print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
     # CPU baseline first: the reference-op leg forks worker processes, which
@@ -294,7 +298,10 @@ def main():
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
 
     if args.global_envs:
         if args.global_envs % world:
@@ -353,7 +360,7 @@ def main():
     lockstep_eff = useful_rhs / (16.0 * wg_sweeps) if wg_sweeps else None
     el_max = elapsed
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev if args.dist_backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el_max = float(t.item())
 
