@@ -204,7 +204,9 @@ def kernel_name(N, part=0):
     groups of `part` oscillators per workgroup when N > 1024)."""
     if N > 1024:
         return f"kura_step_kernel<{(part or 1024) // 256}, true>"
-    return f"kura_step_kernel<{N // 256}, false>"
+    if os.environ.get("KURA_KERNEL") == "k1":   # round-2 kernel, kept for A/B runs
+        return f"kura_step_kernel<{N // 256}, false>"
+    return f"kura_step1w_kernel<{N // 128}, false>"
 
 
 def pmc_traffic(N, B, part=0):

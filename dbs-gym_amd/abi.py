@@ -103,6 +103,9 @@ _SYMBOLS = {
     "kura_step": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                           c_void_p]),
     "kura_reward": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p]),
+    "kura_reward_n": (c_int, [c_void_p, c_int, c_void_p, c_int64, c_int64, c_int, c_void_p, c_void_p, c_int,
+                              c_void_p, c_void_p, c_void_p]),
+    "kura_debug_read_workspace": (c_int, [c_void_p, c_void_p, c_int64]),
     "kura_get_state": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "kura_set_state": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "kura_set_env_gain": (c_int, [c_void_p, c_int, c_int, c_void_p]),

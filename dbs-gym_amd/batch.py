@@ -37,7 +37,10 @@ class EnvHost:
         self.elec_coords = deepcopy(p["elec_coords"])
         self.rec_coords = deepcopy(p["rec_coords"])
         self.encapsulation_coeff = p["conduct_modifier"]                      # env.py:349
-        self.temporal_events = {"electrode_drift": [], "encapsulation_drift": [], "plasticity_drift": []}
+        # env.py:356-359 (logged when save_events; kept here always)
+        self.temporal_events = {"electrode_drift": [], "encapsulation_drift": [], "plasticity_drift": [],
+                                "mov_modulation_drift": []}
+        self.w0 = None                 # kuramoto.w0 of the last reset (env.py:213, :601 kw0)
         if p["temporal_drift"]:                                                # env.py:352-377
             self.random_freq_update = p["random_freq_update"]
             self.elec_drift_episode = p["electrode_drift_freq"]
@@ -99,7 +102,7 @@ class EnvHost:
                 self.plasticity_episode += self._next_event(p["plasticity_drift_freq"], [0, 1])
                 self.w0_without_locus = self.w0_process[self.plasticity_process_count]
                 self.plasticity_process_count += 1
-                self.temporal_events["plasticity_drift"].append([self.reset_count, self.plasticity_process_count])
+                self.temporal_events["plasticity_drift"].append([self.reset_count, deepcopy(self.w0_without_locus)])
             if self.reset_count % self.reset_plasticity_episode == 0:           # env.py:532-541
                 self.plasticity_process_count = 0
                 self.w0_without_locus = deepcopy(self.w0_without_locus_)
@@ -119,6 +122,7 @@ class EnvHost:
             raise AssertionError("Natural frequencies w0 must be positive!")   # env.py:214
         g_stim, g_rec = self._conductances()
         theta0 = ms.initial_phases(self.rs, self.N, p["init_state_mean"], p["init_state_sd"])  # env.py:595-598
+        self.w0 = w0
         return w0, g_stim, g_rec, theta0
 
 

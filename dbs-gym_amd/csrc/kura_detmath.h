@@ -98,10 +98,22 @@ KDM_FN void kdm_sincosf(float x, float* s_out, float* c_out) {
     float cr = KDM_FMAF(z * z, pc, KDM_FMAF(-0.5f, z, 1.0f));
     // quadrant selection without branches (v_cndmask on the GPU):
     // q=0: (s,c) = (sr,cr); 1: (cr,-sr); 2: (-sr,-cr); 3: (-cr,sr)
+#ifdef KURA_BITSEL
+    // variant (r02 bit-select probe): select on bit patterns + sign-bit xor
+    const uint32_t usr = __builtin_bit_cast(uint32_t, sr), ucr = __builtin_bit_cast(uint32_t, cr);
+    const uint32_t odd = (uint32_t)(q & 1);
+    uint32_t us = odd ? ucr : usr;
+    uint32_t uc = odd ? usr : ucr;
+    us ^= ((uint32_t)q & 2u) << 30;
+    uc ^= ((uint32_t)(q + 1) & 2u) << 30;
+    float s = __builtin_bit_cast(float, us);
+    float c = __builtin_bit_cast(float, uc);
+#else
     float s = (q & 1) ? cr : sr;
     float c = (q & 1) ? sr : cr;
     s = (q & 2) ? -s : s;
     c = ((q + 1) & 2) ? -c : c;
+#endif
     *s_out = s;
     *c_out = c;
 }

@@ -201,10 +201,12 @@ __device__ __forceinline__ T* uniform_ptr(T* ptr) {
 }
 
 
-template <int TPW>
+// NWV: waves of the workgroup (8 for K1/K2, 4 for the one-wave-per-SIMD K1w/K2w
+// of kura_k1w.inc); wave w owns column tiles w*TPW .. w*TPW+TPW-1 either way.
+template <int TPW, int NWV = NWAVES>
 __device__ __forceinline__ void coupling_gemm(const float* __restrict__ Xs, const float* __restrict__ alpha_sw,
                                               floatx16 (&acc)[TPW]) {
-    constexpr int N = TPW * 256;
+    constexpr int N = TPW * 32 * NWV;
     constexpr int NK8 = N / 8;
     constexpr int TSTRIDE = NK8 * 64;  // floatx4 per column tile
     // lane id re-derived here (volatile: never CSE'd with a long-lived value),
@@ -392,6 +394,10 @@ struct CtlE {
     int keep, nsave;          // decision of the last attempted step
     int acc_steps, acc_rej;   // over the solves of one launch (stats)
     float t1, tprev, tnext, h, dtn;
+    // K1w (kura_k1w.inc) decides and advances time before the saves of the
+    // step: the save pass reads the step's own save index and interval here
+    int sv_si;
+    float sv_tprev, sv_tnext;
 };
 __shared__ CtlE s_ctl[E_WG];
 __shared__ float s_kn[E_WG];  // per-env coupling gain of the workgroup's envs
@@ -469,6 +475,29 @@ __device__ __forceinline__ void load8(const Slot& w, int slot, int t, float (&v)
         __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(w.rs, w.voff + 1024, w.soff(slot, t), 0));
     split8(a, b, v);
 }
+// Store-data hazard ("The round-2 miscompiles,
+// root-caused").  A buffer_store_dwordx4 reads its four data VGPRs after
+// issue; on gfx950 a VALU write to one of them within the next 2
+// instructions can land first, and the store then writes the NEW value for
+// some lanes (observed: dword 1 of the vector, lanes 12-15 of every 16).
+// LLVM's hazard recognizer inserts those 2 wait states after global / flat /
+// scratch stores, but after a MUBUF store only when its soffset is NOT a
+// register (GCNHazardRecognizer::createsVALUHazard).  Record stores therefore
+// carry their whole offset in the VGPR and soffset = 0, which puts them under
+// the recognizer's guard; the asm makes the lane offset opaque so the
+// per-(slot, tile) adds are not hoisted into long-lived registers.
+// KURA_SGPR_SOFFSET_STORES rebuilds the unguarded form (diagnosis only).
+__device__ __forceinline__ int opaque_vgpr(int v) {
+    asm volatile("" : "+v"(v));
+    return v;
+}
+__device__ __forceinline__ void store_rec_b128(const floatx4& v, __amdgpu_buffer_rsrc_t rs, int voff, int soff) {
+#ifdef KURA_SGPR_SOFFSET_STORES
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u32, v), rs, voff, soff, 0);
+#else
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u32, v), rs, opaque_vgpr(voff) + soff, 0, 0);
+#endif
+}
 __device__ __forceinline__ void store8(const Slot& w, int slot, int t, const float (&v)[8]) {
     // raw buffer stores through the same wave-uniform descriptor as the
     // loads.  Every record is written and read back only by the lane that owns
@@ -478,8 +507,8 @@ __device__ __forceinline__ void store8(const Slot& w, int slot, int t, const flo
     // N=256 during development; it does not reproduce at the commit that
     // introduced the workaround or at any later one)
     const floatx4 a = {v[0], v[1], v[2], v[3]}, b = {v[4], v[5], v[6], v[7]};
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u32, a), w.rs, w.voff, w.soff(slot, t), 0);
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u32, b), w.rs, w.voff + 1024, w.soff(slot, t), 0);
+    store_rec_b128(a, w.rs, w.voff, w.soff(slot, t));
+    store_rec_b128(b, w.rs, w.voff + 1024, w.soff(slot, t));
 }
 
 // f = fmaf(kn, fmaf(c, P, -(s*Q)), omega) + pulse  ->  slot F0 + stage
@@ -1411,13 +1440,15 @@ __device__ void filtfilt_last_wave(const DevParams& p, const WinView (&xv)[NF], 
 
 // Reward of the window held in registers (R64 layout), env.py:638-688.
 // Must be called by the whole wave (the DFT reductions shuffle).
-template <int WPL>
-__device__ double reward_of(const DevParams& p, const double (&x)[WPL], double u0, const WinView& xv, double* ext,
-                            double* tmp, const double* d_pre = nullptr) {
+// PRE: the R2 filter term d is given (*d_pre, the step kernels' r2_filters);
+// otherwise it is computed here (the standalone reward kernel).
+template <int WPL, bool PRE = false>
+__device__ __forceinline__ double reward_of(const DevParams& p, const double (&x)[WPL], double u0, const WinView& xv,
+                                            double* ext, double* tmp, const double* d_pre = nullptr) {
     const double au = fabs(u0);
     if (p.reward_kind == KURA_R_TEMP_CONST) {
         double d[1];
-        if (d_pre) {
+        if (PRE) {
             d[0] = *d_pre;
         } else {
             const WinView v1[1] = {xv};
@@ -1692,7 +1723,7 @@ __device__ __forceinline__ void step_pair(const DevParams& p, Part& pt, float* X
         }
         double* ext = p.scratch + (size_t)env * 2 * (W + 2 * p.padlen);
         double* tmp = ext + (W + 2 * p.padlen);
-        const double r = reward_of<WPL>(p, x, s_u[e][0], xv, ext, tmp, r2 ? &r2d[ee] : nullptr);
+        const double r = reward_of<WPL, true>(p, x, s_u[e][0], xv, ext, tmp, &r2d[ee]);
         // ring append after every read of the old slots
         if (lane < S) {
             int k = wp0 + lane;
@@ -1841,6 +1872,56 @@ __global__ __launch_bounds__(64) void kura_reward_kernel(DevParams p, const doub
     if (lane == 0) out[env] = r;
 }
 
+// ------------------------------------------- reward on any window length --
+// reward_* of env.py:638-688 on 1-D windows of any length L (the reference
+// computes the beta bins from len(x_state), utils.py:21-27, e.g. the n_envs*W
+// samples PIDController.predict passes, aDBS_RL/agents/simple_dbs.py:81-88).
+// One wave per window, read from memory: R1/R3 = the bins' R64 dots against
+// host twiddle rows of length L (the same R64 order as window_dot, so a
+// length-W call equals kura_reward bit for bit), R2 = filtfilt_last_wave on
+// the window with p.W = L.
+__global__ __launch_bounds__(64) void kura_reward_n_kernel(DevParams p, const double* __restrict__ x, long long ld,
+                                                           const double* __restrict__ ctab,
+                                                           const double* __restrict__ stab, int n_bins,
+                                                           const float* __restrict__ u0, double* __restrict__ out,
+                                                           double* __restrict__ scratch, int n) {
+    const int j = blockIdx.x;
+    if (j >= n) return;
+    const int lane = threadIdx.x;
+    const int L = p.W;
+    const double* xw = x + (size_t)j * ld;
+    const double au = fabs((double)u0[j]);
+    double r;
+    if (p.reward_kind == KURA_R_TEMP_CONST) {
+        const WinView v1[1] = {WinView{xw, 0, L, 0, 0}};
+        double* const e1[1] = {scratch + (size_t)j * 2 * (L + 2 * p.padlen)};
+        double* const t1[1] = {e1[0] + (L + 2 * p.padlen)};
+        double d[1];
+        filtfilt_last_wave<1>(p, v1, e1, t1, d);
+        r = -(1e3 * (d[0] * d[0])) - 1e-2 * au;
+    } else {
+        double bb = 0.0;
+        for (int b = 0; b < n_bins; ++b) {
+            double re = 0.0, im = 0.0;
+            for (int i = lane; i < L; i += 64) {
+                re = __builtin_fma(xw[i], ctab[(size_t)b * L + i], re);
+                im = __builtin_fma(xw[i], stab[(size_t)b * L + i], im);
+            }
+            re = wave_sum_f64(re);
+            im = wave_sum_f64(im);
+            const double pr = re / (double)L, pi = im / (double)L;
+            bb = bb + (pr * pr + pi * pi) * 2.0;
+        }
+        if (p.reward_kind == KURA_R_BBPOW_THR) {
+            r = -(1e4 * bb > 20.0 ? 5.0 : 0.0) - au;
+        } else {
+            r = -(1e4 * bb) - 1e-2 * au;
+        }
+    }
+    if (lane == 0) out[j] = r;
+}
+
+#include "kura_k1w.inc"
 #include "kura_fft.inc"
 
 // ------------------------------------------------------------- self-tests --

@@ -4,12 +4,13 @@
 table, ``data/kur-table-metrics.xlsx``) runs, in ONE process with the global
 NumPy RNG:
 
-1. ``np.random.seed(228)`` (:20), then ``generate_w0_with_locus`` for each of
-   the five eval configs in order (:204-213) -- env k's frequencies depend on
-   the draws made for envs 0..k-1;
-2. ``SpatialKuramoto(params)`` for each config (:225): the constructor reseeds
-   the global RNG with the config's ``rand_seed`` (env.py:291), draws env2's
-   plasticity walk (env.py:375-377) and runs ``reset()`` once (env.py:386);
+1. ``np.random.seed(228)`` (:20);
+2. for each of the five eval configs in turn (:195-218): ``generate_w0_with_locus``
+   from the global RNG (:198-205), then ``make_env`` = ``SpatialKuramoto(params)``
+   (:23-30, :218), whose constructor reseeds the global RNG with the config's
+   ``rand_seed`` (env.py:291), draws env2's plasticity walk (env.py:375-377)
+   and runs ``reset()`` once (env.py:386) -- so env k+1's frequencies come
+   from the RNG state env k's constructor left behind;
 3. ``evaluate_policy_`` env by env (:138-151): ``DummyVecEnv.reset()`` and one
    autoreset after every finished episode, the last one included, each
    ``reset()`` drawing from the same global RNG (env.py:483-598);
@@ -45,33 +46,24 @@ class ReplayHost:
         return self.draws[self.reset_count]
 
 
-def protocol_params(name: str, n_envs: int = 5, seed: int = 228, rs: np.random.RandomState | None = None,
-                    reward_func: str = "bbpow_action", **overrides):
-    """Step 1 of the protocol: the eval params dicts with their driver arrays
-    (evaluate_HF_DBS.py:198-221), drawn from one RNG seeded with ``seed``;
-    ``overrides`` update every dict (e.g. encapsulation_mode="relative")."""
-    rs = rs if rs is not None else np.random.RandomState()
-    rs.seed(seed)
-    plist = []
-    for k in range(n_envs):
-        p = reference_params(name, "eval", k, **overrides)
-        p["reward_func"] = reward_func                                        # :215
-        p["dbs_action_bounds"] = [-5, 5]                                      # :224
-        plist.append(fill_driver_arrays(p, rs=rs))
-    return plist, rs
-
-
-def protocol_draws(name: str, n_episodes: int, n_envs: int = 5, seed: int = 228, **overrides):
+def protocol_draws(name: str, n_episodes: int, n_envs: int = 5, seed: int = 228,
+                   rs: np.random.RandomState | None = None, reward_func: str = "bbpow_action", **overrides):
     """Steps 1-3: returns (params list, per-env list of reset draws) where
     draws[k][0] is the constructor's reset (its transient is discarded by the
     script) and draws[k][1:] the n_episodes + 1 resets of evaluate_policy_
-    (the DummyVecEnv reset, then one autoreset per finished episode)."""
-    plist, rs = protocol_params(name, n_envs, seed, **overrides)
-    hosts = []
-    draws = []
-    for p in plist:                      # SpatialKuramoto(...) for each config, in order
-        h = EnvHost(p, rs=rs)
-        draws.append([h.reset_draws()])  # env.py:386
+    (the DummyVecEnv reset, then one autoreset per finished episode);
+    ``overrides`` update every params dict (e.g. encapsulation_mode="relative")."""
+    rs = rs if rs is not None else np.random.RandomState()
+    rs.seed(seed)                                                               # :20
+    plist, hosts, draws = [], [], []
+    for k in range(n_envs):              # generate_w0_with_locus, then make_env, config by config
+        p = reference_params(name, "eval", k, **overrides)
+        p["reward_func"] = reward_func                                        # :207
+        p["dbs_action_bounds"] = [-5, 5]                                      # :216
+        p = fill_driver_arrays(p, rs=rs)                                      # :198-214
+        h = EnvHost(p, rs=rs)                                                 # :218 -> env.py:291
+        draws.append([h.reset_draws()])                                       # env.py:386
+        plist.append(p)
         hosts.append(h)
     for h, d in zip(hosts, draws):       # evaluate_policy_ env by env
         for _ in range(n_episodes + 1):
@@ -132,4 +124,4 @@ def run_protocol(name: str, actions=(0.0, 1.0), n_episodes: int = 5, n_envs: int
             "actions": list(actions)}
 
 
-__all__ = ["ReplayHost", "protocol_params", "protocol_draws", "run_protocol"]
+__all__ = ["ReplayHost", "protocol_draws", "run_protocol"]

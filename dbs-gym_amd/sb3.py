@@ -32,7 +32,7 @@ _REWARD_METHODS = ("reward_bbpow_action", "reward_temp_const_lfp_betafilt_action
 
 
 class KuraSB3VecEnv:
-    def __init__(self, venv: KuraVectorEnv, monitor: bool = True, obs_buffers: int | None = 4):
+    def __init__(self, venv: KuraVectorEnv, monitor: bool = True, obs_buffers: int | None = None):
         if not venv.autoreset:
             raise ValueError("KuraSB3VecEnv needs a KuraVectorEnv with autoreset=True (DummyVecEnv semantics)")
         self.venv = venv
@@ -46,12 +46,12 @@ class KuraSB3VecEnv:
         self._ep_len = np.zeros(self.num_envs, np.int64)
         self._t0 = np.full(self.num_envs, time.time())
         self._pin = None   # pinned host staging for the per-step device -> host copies
-        # observations are returned in a ring of obs_buffers preallocated host
-        # arrays (an array stays valid for obs_buffers - 1 further steps --
-        # SB3's rollout collection and evaluate_policy copy or drop it after
-        # one); None returns a fresh array every step, DummyVecEnv's exact
-        # semantics, at ~2x the host cost per step (page faults of a new
-        # (B, 1, W) array, tools/sb3_bench.py)
+        # None (default): a fresh observation array every step, DummyVecEnv's
+        # semantics (callers may keep references).  obs_buffers = k (opt-in):
+        # a ring of k preallocated host arrays -- an array stays valid for
+        # k - 1 further steps (SB3's rollout collection and evaluate_policy
+        # copy or drop it after one) -- at ~half the host cost per step (no
+        # page faults of a new (B, 1, W) array, tools/sb3_bench.py)
         self.obs_buffers = obs_buffers
         self._ring, self._ring_i = None, 0
 
@@ -135,11 +135,12 @@ class KuraSB3VecEnv:
         self.venv.close()
 
     def seed(self, seed=None):
-        """SB3 VecEnv.seed: env i gets seed + i at the next reset (np.random.seed per env)."""
+        """SB3 VecEnv.seed: env i is reset with seed + i at the next reset, which
+        seeds only its gymnasium np_random (env.py:471); the reference's draws
+        come from the global NumPy RNG and continue their streams."""
         if seed is None:
             return [None] * self.num_envs
-        for i, h in enumerate(self.venv.hosts):
-            h.rs.seed(int(seed) + i)
+        self.venv.np_random = [np.random.default_rng(int(seed) + i) for i in range(self.num_envs)]
         return [int(seed) + i for i in range(self.num_envs)]
 
     # ---- attribute / method access ------------------------------------------------
@@ -154,11 +155,8 @@ class KuraSB3VecEnv:
         return self.venv.get_attr(attr_name, self._idx(indices))
 
     def set_attr(self, attr_name: str, value, indices=None) -> None:
-        for i in self._idx(indices):
-            if attr_name == "params_dict":
-                self.venv.params[i] = value
-            else:
-                raise AttributeError(f"set_attr({attr_name!r}) is not supported on the batched env")
+        """SB3 VecEnv.set_attr: takes effect (KuraVectorEnv.set_attr) or raises."""
+        self.venv.set_attr(attr_name, value, self._idx(indices))
 
     def env_method(self, method_name: str, *args, indices=None, **kwargs):
         """The reference env methods callers invoke through a VecEnv: the three

@@ -280,6 +280,29 @@ class KuraSim:
                                                 st["wpos"].ctypes.data), "kura_get_state")
         return st
 
+    def times(self) -> np.ndarray:
+        """current_time of every env (env.py:431,441,609), float64 (syncs)."""
+        t = np.empty(self.B, np.float64)
+        check(self.lib, self.lib.kura_get_state(self._h, None, t.ctypes.data, None, None, None), "kura_get_state")
+        return t
+
+    def reward_n(self, x: torch.Tensor, u0: torch.Tensor, kind: int, cos_tab, sin_tab) -> torch.Tensor:
+        """reward_* of n windows of any length L (x: (n, L)); twiddles (n_bins, L)
+        for that length (kura_reward_n)."""
+        w = x.to(self.device, torch.float64).contiguous()
+        u = u0.to(self.device, torch.float32).contiguous()
+        n, L = w.shape
+        ct = torch.as_tensor(np.ascontiguousarray(cos_tab, np.float64), device=self.device)
+        st = torch.as_tensor(np.ascontiguousarray(sin_tab, np.float64), device=self.device)
+        nb = int(ct.shape[0]) if ct.ndim == 2 else 0
+        out = torch.empty(n, dtype=torch.float64, device=self.device)
+        with torch.cuda.device(self.device):
+            check(self.lib, self.lib.kura_reward_n(self._h, int(kind), ptr(w), L, L, n, ptr(ct) if nb else None,
+                                                   ptr(st) if nb else None, nb, ptr(u), ptr(out), self._stream()),
+                  "kura_reward_n")
+        self._keep_rw = (w, u, ct, st)
+        return out
+
     def set_state(self, st: dict) -> None:
         arrs = [np.ascontiguousarray(st["y"], np.float32), np.ascontiguousarray(st["t"], np.float64),
                 np.ascontiguousarray(st["step"], np.int32), np.ascontiguousarray(st["ring"], np.float64),

@@ -14,7 +14,9 @@ torch tensors unless the caller asks for NumPy.
 from __future__ import annotations
 
 import copy
+import os
 import time
+from types import SimpleNamespace
 
 import numpy as np
 import torch
@@ -63,7 +65,16 @@ class KuraVectorEnv:
                 diffeqsolve does (diffrax throw=True, env.py:261-270);
                 "reset" reports the env terminated + truncated with
                 ``infos["failed_env_ids"]``/``infos["failure_flags"]`` and
-                autoresets it.
+                autoresets it; an autoreset whose transient fails is reported
+                in ``infos["failed_reset_ids"]`` and retried, up to
+                ``max_reset_failures`` times in a row per env, then raises.
+    failure_check: "deferred" (default) -- the library's per-env failure
+                flags of a launch travel to the host by an asynchronous copy
+                into pinned memory and are acted on at the start of the next
+                step() (before its launch), so a step never blocks on the
+                device; a failed env reports done = 1 in the step it failed
+                (the kernel's own output) and is raised / reset one call later.
+                "eager": every step() synchronises and acts at once.
     """
 
     metadata = {"render.modes": ["human"]}
@@ -71,10 +82,15 @@ class KuraVectorEnv:
     def __init__(self, params, num_envs: int | None = None, device=0, reward_func: str | None = None,
                  w0_seed: int = 228, rand_seeds=None, autoreset: bool = True, max_steps: int = 4096,
                  episode_metrics: bool = False, psd_dt: float = 5e-4, beta_band=(12.5, 21.0),
-                 on_failure: str = "raise", profile: bool = False):
+                 on_failure: str = "raise", profile: bool = False, failure_check: str = "deferred",
+                 max_reset_failures: int = 3):
         if on_failure not in ("raise", "reset"):
             raise ValueError(f"on_failure={on_failure!r}: expected 'raise' or 'reset'")
+        if failure_check not in ("deferred", "eager"):
+            raise ValueError(f"failure_check={failure_check!r}: expected 'deferred' or 'eager'")
         self.on_failure = on_failure
+        self.failure_check = failure_check
+        self.max_reset_failures = int(max_reset_failures)
         self.profile = profile
         self.boundary_times: list[dict] = []
         if isinstance(params, dict):
@@ -116,6 +132,15 @@ class KuraVectorEnv:
         self.steps = np.zeros(B, np.int64)
         self.episode_steps = self.cfg.episode_steps
         self.u = torch.zeros((B, self.n_elec), dtype=torch.float64, device=self.device)
+        self._alpha = shared["alpha"]                                # float64, env.py:219-229 (kuramoto.alpha)
+        self._gain = shared["gain"]
+        # gymnasium Env.reset(seed) only seeds the env's own np_random, which
+        # SpatialKuramoto never draws from (env.py:471): kept for callers
+        self.np_random = [None] * B
+        # deferred failure flags: pinned host copies of the last step's and the
+        # last autoreset's per-env flags, and the events that complete them
+        self._pend = None          # (flags_pinned, event, reset_mask or None, reset_flags_pinned)
+        self._reset_fail_runs = np.zeros(B, np.int64)
         self._omega = np.zeros((B, self.N), np.float32)
         self._g_stim = np.zeros((B, self.n_elec, self.N))
         self._g_rec = np.zeros((B, max(self.cfg.n_rec, 1), self.N))
@@ -130,6 +155,7 @@ class KuraVectorEnv:
         th = np.zeros((self.num_envs, self.N), np.float32)
         for b in idx:
             w0, gs, gr, th0 = self.hosts[b].reset_draws()
+            self._log_events(b)
             self._omega[b] = w0.astype(np.float32)
             self._g_stim[b] = gs
             self._g_rec[b] = gr
@@ -149,19 +175,71 @@ class KuraVectorEnv:
         self._t_upload = time.perf_counter() - t0 - self._t_draw
         return out
 
+    def _log_events(self, b):
+        """env.py:559-562: with save_events and a log_path, every reset after the
+        second saves the env's temporal events to log_path/temp_<reset_count>.npy
+        (np.save of the dict; the reference keeps temporal_events only for
+        temporal-drift configs and raises AttributeError otherwise)."""
+        p, h = self.params[b], self.hosts[b]
+        if p.get("save_events") and p.get("log_path") is not None and h.reset_count > 1:
+            if not p.get("temporal_drift"):
+                raise AttributeError("'SpatialKuramoto' object has no attribute 'temporal_events'")
+            np.save(os.path.join(p["log_path"], f"temp_{h.reset_count}.npy"), h.temporal_events,
+                    allow_pickle=True)
+
     def reset(self, seed=None, options=None):
-        """env.py:467-614 for every env.  ``seed`` (int or list) reseeds the
-        per-env RNG streams before the draws, like np.random.seed."""
+        """env.py:467-614 for every env.  ``seed`` (int or list) seeds each
+        env's gymnasium ``np_random`` only (env.py:471 super().reset(seed)); the
+        reference's draws come from the global NumPy RNG, which reset(seed)
+        does not touch, so they continue their streams."""
         if seed is not None:
             seeds = [seed + b for b in range(self.num_envs)] if np.isscalar(seed) else list(seed)
-            for h, s in zip(self.hosts, seeds):
-                h.rs.seed(int(s))
+            self.np_random = [np.random.default_rng(int(x)) for x in seeds]
+        self._pend = None
         th = self._draw(range(self.num_envs))
         obs = self.sim.reset(th)
         self._check_reset(None)
         self.steps[:] = 0
         self._was_reset = True
         return obs.view(self.num_envs, 1, self.W).clone(), {}
+
+    def _failures_now(self):
+        """Flags of the last launch, synchronously."""
+        return self.sim.failed_envs()
+
+    def _take_pending(self):
+        """The deferred flags of the previous step (and of its autoreset):
+        (failed env ids, flags, failed reset ids).  Waits only for the copies,
+        which the previous launches completed long ago in a stepping loop."""
+        if self._pend is None:
+            return np.zeros(0, np.int64), np.zeros(0, np.int32), np.zeros(0, np.int64)
+        fl, ev, rmask, rfl = self._pend
+        self._pend = None
+        ev.synchronize()
+        f = fl.numpy().copy()
+        idx = np.nonzero(f)[0]
+        ridx = np.zeros(0, np.int64)
+        if rmask is not None:
+            rf = np.where(rmask, rfl.numpy(), 0)
+            ridx = np.nonzero(rf)[0]
+        return idx, f[idx], ridx
+
+    def _stash_flags(self, reset_mask=None):
+        """Start the asynchronous copy of the last launch's flags (step, or the
+        autoreset that followed it) into pinned memory."""
+        if self._pend is None or reset_mask is None:
+            fl = torch.empty(self.num_envs, dtype=torch.int32, pin_memory=True)
+            fl.copy_(self.sim.flags, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(self.device))
+            self._pend = (fl, ev, None, None)
+        else:
+            fl, _, _, _ = self._pend
+            rfl = torch.empty(self.num_envs, dtype=torch.int32, pin_memory=True)
+            rfl.copy_(self.sim.flags, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(self.device))
+            self._pend = (fl, ev, reset_mask, rfl)
 
     def step(self, actions):
         """env.py:415-454 for every env; returns (obs (B,1,W), rewards (B,),
@@ -170,23 +248,31 @@ class KuraVectorEnv:
             raise RuntimeError("reset() must be called before step()")
         a = torch.as_tensor(np.asarray(actions, np.float32) if not torch.is_tensor(actions) else actions,
                             device=self.device, dtype=torch.float32).reshape(self.num_envs, self.n_elec)
+        infos: dict = {}
+        # the previous step's deferred failures (and its autoreset's), before this launch
+        pre_failed, pre_flags, pre_rfail = self._take_pending()
+        if len(pre_failed) or len(pre_rfail):
+            self._act_on_failures(pre_failed, pre_flags, pre_rfail, infos, "kura_step (previous call)")
         lo, hi = self.cfg.dbs_lo, self.cfg.dbs_hi
-        self.u = lo + ((hi - lo) * (a.double() + 1.0)) / 2.0        # env.py:389-393 (for callers)
+        x, y = self.cfg.act_lo, self.cfg.act_hi
+        self.u = lo + ((hi - lo) * (a.double() - x)) / (y - x)      # env.py:389-393 (for callers)
         obs, rew, done = self.sim.step(a)
         self.steps += 1
-        infos: dict = {}
         term_host = self.steps >= self.episode_steps
         terminated = done.bool().clone()
         truncated = torch.zeros_like(terminated)
-        failed, fflags = self.sim.failed_envs()          # synchronises: the step's outputs are ready
-        if len(failed):
-            if self.on_failure == "raise":
-                raise KuraSolverError("kura_step", failed.tolist(), fflags.tolist())
-            infos["failed_env_ids"] = failed
-            infos["failure_flags"] = fflags
-            truncated[torch.as_tensor(failed, device=self.device)] = True
-            term_host = term_host.copy()
-            term_host[failed] = True                     # autoreset keys on the same envs the flags name
+        if self.failure_check == "eager":
+            failed, fflags = self._failures_now()         # synchronises: the step's outputs are ready
+            if len(failed):
+                if self.on_failure == "raise":
+                    raise KuraSolverError("kura_step", failed.tolist(), fflags.tolist())
+                infos["failed_env_ids"] = failed
+                infos["failure_flags"] = fflags
+                truncated[torch.as_tensor(failed, device=self.device)] = True
+                term_host = term_host.copy()
+                term_host[failed] = True                 # autoreset keys on the same envs the flags name
+        else:
+            self._stash_flags()
         tb = {}
         if term_host.any():
             t0 = time.perf_counter()
@@ -209,7 +295,10 @@ class KuraVectorEnv:
             th = self._draw(idx)
             t1 = time.perf_counter()
             self.sim.reset(th, mask.to(self.device))
-            self._check_reset(mask)
+            if self.failure_check == "eager":
+                self._check_reset(mask)
+            else:
+                self._stash_flags(reset_mask=mask.numpy().astype(bool))
             if self.profile:
                 torch.cuda.synchronize(self.device)
             self.steps[idx] = 0
@@ -219,9 +308,56 @@ class KuraVectorEnv:
             self.boundary_times.append(tb)
         return obs.view(self.num_envs, 1, self.W).clone(), rew.clone(), terminated, truncated, infos
 
-    def _check_reset(self, mask):
+    def _check_reset(self, mask, infos=None):
+        """Synchronous check of a reset launch: raise, or (on_failure='reset')
+        report the failed envs and reset them again."""
         if self.on_failure == "raise":
             self.sim.raise_on_failure("kura_reset", None if mask is None else mask.to(self.device))
+            return
+        ridx, _ = self.sim.failed_envs(None if mask is None else mask.to(self.device))
+        if len(ridx):
+            self._retry_resets(ridx, infos if infos is not None else {})
+
+    def _retry_resets(self, ridx, infos):
+        self._reset_fail_runs[ridx] += 1
+        over = ridx[self._reset_fail_runs[ridx] > self.max_reset_failures]
+        if len(over):
+            raise KuraSolverError("kura_reset (repeated)", over.tolist(), [0] * len(over))
+        infos["failed_reset_ids"] = np.asarray(ridx)
+        mask = torch.zeros(self.num_envs, dtype=torch.uint8)
+        mask[ridx] = 1
+        th = self._draw(ridx)
+        self.sim.reset(th, mask.to(self.device))
+        self.steps[ridx] = 0
+        self._check_reset(mask, infos)
+
+    def _act_on_failures(self, failed, fflags, rfailed, infos, what):
+        """Deferred failures of the previous call: raise, or report them and
+        reset those envs now (before this step's launch)."""
+        if self.on_failure == "raise":
+            if len(failed):
+                raise KuraSolverError(what, failed.tolist(), fflags.tolist())
+            raise KuraSolverError("kura_reset (autoreset of the previous call)", rfailed.tolist(),
+                                  [0] * len(rfailed))
+        ok = np.setdiff1d(np.arange(self.num_envs), rfailed)
+        self._reset_fail_runs[ok] = 0
+        if len(failed):
+            infos["failed_env_ids"] = failed
+            infos["failure_flags"] = fflags
+        redo = np.union1d(failed, rfailed).astype(np.int64)
+        if len(rfailed):
+            self._reset_fail_runs[rfailed] += 1
+            over = rfailed[self._reset_fail_runs[rfailed] > self.max_reset_failures]
+            if len(over):
+                raise KuraSolverError("kura_reset (repeated)", over.tolist(), [0] * len(over))
+            infos["failed_reset_ids"] = rfailed
+        if len(redo):
+            mask = torch.zeros(self.num_envs, dtype=torch.uint8)
+            mask[redo] = 1
+            th = self._draw(redo)
+            self.sim.reset(th, mask.to(self.device))
+            self.steps[redo] = 0
+            self._check_reset(mask, infos)
 
     # ---- attributes read by the reference's callers ----------------------------
     @property
@@ -233,9 +369,30 @@ class KuraVectorEnv:
     def theta_records(self):
         return self.sim.lfp_rec, self.sim.nsamp
 
+    def kuramoto_view(self, b):
+        """The attributes of env b's KuramotoJAX / SimpleDBS (env.py:191-249,
+        :61-156) that callers read, e.g. ``env.kuramoto.dbs.conductances``
+        (explore_kuramoto_dynamics.ipynb cell 13): the last reset's values."""
+        p, h = self.params[b], self.hosts[b]
+        gs, gr = h._conductances() if hasattr(h, "_conductances") else (None, None)
+        dbs = SimpleNamespace(conductances=None if gs is None else [np.array(g) for g in gs],
+                              rec_conductances=None if gr is None else [np.array(g) for g in gr],
+                              elec_coords=getattr(h, "elec_coords", p["elec_coords"]),
+                              rec_coords=getattr(h, "rec_coords", p["rec_coords"]))
+        return SimpleNamespace(K=p["K"], n_neurons=p["num_oscillators"], w0=getattr(h, "w0", None),
+                               grid_size=p["grid_size"], neur_coords=p["neur_coords"], neur_grid=p["neur_grid"],
+                               spatial_kernel=p["spatial_kernel"], alpha=self._alpha, dbs=dbs,
+                               pulse=np.zeros(p["num_oscillators"]))
+
+    # attributes of SpatialKuramoto (env.py:277-614) served by get_attr
+    _HOST_ATTRS = ("reset_count", "temporal_events", "spatial_events", "elec_coords", "rec_coords",
+                   "encapsulation_coeff", "w0_without_locus")
+
     def get_attr(self, name: str, indices=None):
-        """SB3 VecEnv.get_attr for the attributes the reference callers read
-        (evaluate_HF_DBS.py:83, custom_callbacks.py:132-134,302)."""
+        """SB3 VecEnv.get_attr for the attributes of the reference env that its
+        callers read (evaluate_HF_DBS.py:83, custom_callbacks.py:107-134,302,
+        the notebooks' env.kuramoto.dbs.conductances) and the bookkeeping
+        reset() sets (env.py:473-476, :600-603)."""
         idx = range(self.num_envs) if indices is None else indices
         if name in ("theta_mean", "theta_records"):
             vals, n = (self.sim.lfp_true if name == "theta_mean" else self.sim.lfp_rec), self.sim.nsamp
@@ -248,14 +405,81 @@ class KuraVectorEnv:
             return [self.params[i] for i in idx]
         if name == "current_step":
             return [int(self.steps[i]) for i in idx]
+        if name == "current_time":
+            t = self.sim.times()
+            return [float(t[i]) for i in idx]
+        if name == "theta_state":
+            o = self.sim.obs.cpu().numpy()
+            return [o[i][None, :].astype(np.float32) for i in idx]
+        if name == "done":
+            return [bool(self.steps[i] >= self.episode_steps) for i in idx]
+        if name == "kuramoto":
+            return [self.kuramoto_view(i) for i in idx]
+        if name == "kw0":                                           # env.py:601
+            return [self.hosts[i].w0 for i in idx]
+        if name == "kneur_grid":                                    # env.py:602
+            return [self.params[i]["neur_grid"] for i in idx]
+        if name == "kgrid_size":                                    # env.py:603
+            return [self.params[i]["grid_size"] for i in idx]
+        if name in self._HOST_ATTRS:
+            return [getattr(self.hosts[i], name) for i in idx]
+        if name == "np_random":
+            return [self.np_random[i] for i in idx]
         raise AttributeError(name)
 
+    # params the batch is built around: they cannot change on a running handle
+    _FIXED_KEYS = ("num_oscillators", "grid_size", "neur_coords", "neur_grid", "spatial_kernel", "wavelet_amp",
+                   "wavelet_steepness", "electrode_width", "electrode_pause", "verbose_dt", "observe_wind_counts",
+                   "total_episode_len", "transient_state_len", "reward_func", "recording_kernel",
+                   "dbs_action_bounds")
+
+    def set_attr(self, name: str, value, indices=None) -> None:
+        """SB3 VecEnv.set_attr.  ``params_dict`` takes effect from the next
+        reset of those envs (the reference reads its params_dict there, and K
+        at every solve, env.py:264): per-reset draws, drift/spatial settings
+        and K follow the new dict; keys the batch's shared setup is built on
+        (N, grid, window, timing, reward, kernels) must stay equal or
+        ValueError is raised.  Other names raise AttributeError."""
+        idx = list(range(self.num_envs)) if indices is None else list(indices)
+        if name != "params_dict":
+            raise AttributeError(f"set_attr({name!r}) is not supported on the batched env")
+        for i in idx:
+            old = self.params[i]
+            for k in self._FIXED_KEYS:
+                a, b = old.get(k), value.get(k)
+                same = np.array_equal(np.asarray(a), np.asarray(b)) if isinstance(a, (list, tuple, np.ndarray)) \
+                    else a == b
+                if not same:
+                    raise ValueError(f"set_attr('params_dict'): {k!r} cannot change on a running batch "
+                                     "(build a new env)")
+            newp = copy.deepcopy(value)
+            for k in ("w0", "w0_without_locus", "locus_without_w0", "locus_mask"):
+                if newp.get(k) is None:
+                    newp[k] = old.get(k)
+            self.params[i] = newp
+            self.hosts[i].p = newp
+            if newp["K"] != old["K"]:
+                self._gain[i] = np.float32(newp["K"] / newp["num_oscillators"])
+                self.sim.set_env_gain(self._gain[i:i + 1], env0=i)
+
     def reward_of(self, windows, u0, kind: int = 0):
-        """reward_* (env.py:638-688) of given windows (n, W) and first amplitudes u0
-        (kind: 1 bbpow_action, 2 temp_const_action, 3 bbpow_threth_action, 0 = config's)."""
+        """reward_* (env.py:638-688) of given 1-D windows (n, L) of any length L
+        and first amplitudes u0 (kind: 1 bbpow_action, 2 temp_const_action,
+        3 bbpow_threth_action, 0 = config's).  The beta bins follow len(x)
+        as in the reference (utils.py:21-27)."""
         w = torch.as_tensor(np.asarray(windows, np.float64), device=self.device)
-        u = torch.as_tensor(np.asarray(u0, np.float32), device=self.device)
-        return self.sim.reward_of(w.reshape(-1, self.W), u.reshape(-1), kind)
+        w = w.reshape(1, -1) if w.ndim == 1 else w.reshape(w.shape[0], -1)
+        u = torch.as_tensor(np.asarray(u0, np.float32), device=self.device).reshape(-1)
+        L = int(w.shape[1])
+        if L == self.W:
+            return self.sim.reward_of(w, u, kind)
+        kind = kind or self.cfg.reward_kind
+        bins = spectral.beta_bins(L, self.params[0]["verbose_dt"])
+        ct, st = spectral.twiddles(L, bins) if len(bins) else (np.zeros((0, L)), np.zeros((0, L)))
+        if kind == 2 and L <= self.cfg.padlen:
+            raise ValueError(f"The length of the input vector x must be greater than padlen, which is "
+                             f"{self.cfg.padlen}.")
+        return self.sim.reward_n(w, u, kind, ct, st)
 
     def state_dict(self):
         """Checkpointable env state (phases, times, counters, windows)."""
@@ -288,7 +512,7 @@ class SpatialKuramoto:
                                       "undefined init_state on the first reset, env.py:594)")
         self.params_dict = params_dict
         self._v = KuraVectorEnv([params_dict], device=device, rand_seeds=[params_dict["rand_seed"]],
-                                autoreset=False)
+                                autoreset=False, failure_check="eager")
         self._v.sim.capture_rows(True)          # sol_state_: every row of the step (env.py:430,440)
         self.action_space = self._v.single_action_space
         self.observation_space = self._v.single_observation_space
@@ -297,9 +521,9 @@ class SpatialKuramoto:
         self.reset()
 
     def reset(self, seed=None, options=None):
-        if seed is not None:
-            self._v.hosts[0].rs.seed(int(seed))
-        obs, info = self._v.reset()
+        """env.py:467-614.  ``seed`` seeds gymnasium's np_random only
+        (env.py:471): the draws continue the env's global-RNG stream."""
+        obs, info = self._v.reset(seed=None if seed is None else [int(seed)])
         self.current_step = 0
         self.done = False
         self.theta_state = obs[0].cpu().numpy()
@@ -317,6 +541,32 @@ class SpatialKuramoto:
         self.reward_ = float(rew[0].item())
         return self.theta_state.astype(np.float32), self.reward_, self.done, False, {}
 
+    # reference attributes set by __init__/reset()/step() (env.py:289, :473-476,
+    # :600-603) and the model objects (env.py:570-593): served by the batch
+    @property
+    def reset_count(self):
+        return self._v.hosts[0].reset_count
+
+    @property
+    def current_time(self):
+        return self._v.get_attr("current_time")[0]
+
+    @property
+    def kuramoto(self):
+        return self._v.kuramoto_view(0)
+
+    @property
+    def np_random(self):
+        return self._v.np_random[0]
+
+    def __getattr__(self, name):
+        # only reached for names not set on the instance / class
+        if name.startswith("_"):
+            raise AttributeError(name)
+        if name in ("kw0", "kneur_grid", "kgrid_size") + KuraVectorEnv._HOST_ATTRS:
+            return self._v.get_attr(name)[0]
+        raise AttributeError(f"'SpatialKuramoto' object has no attribute {name!r}")
+
     @property
     def sol_state_(self):
         """Every saved phase row of the last step, ys_I then ys_II (env.py:430,440): (nsamp + 1, N) float32."""
@@ -324,6 +574,7 @@ class SpatialKuramoto:
         return self._v.sim.rows[0, :n + 1].cpu().numpy()
 
     def _reward(self, kind, x_state, action_value):
+        """Any 1-D length (the bins follow len(x_state), utils.py:21-27)."""
         assert len(np.asarray(x_state).shape) == 1, "Incorrect dimension of theta_state"
         return float(self._v.reward_of(np.asarray(x_state)[None, :], [action_value[0]], kind)[0].item())
 

@@ -7,8 +7,11 @@
  * pointers are DEVICE pointers allocated by the caller (PyTorch-ROCm tensors
  * via tensor.data_ptr()); they are borrowed for the duration of the call and
  * the work is enqueued on the given hipStream_t (NULL = default stream).
- * Setup calls take HOST pointers and are synchronous.  No call allocates
- * device memory except kura_create.  Errors never throw across the ABI: every
+ * Setup calls take HOST pointers and are synchronous.  kura_step and
+ * kura_reset never allocate device memory (kura_create does it once); the
+ * episode-metric calls grow a per-handle scratch on demand and kura_reward_n
+ * takes stream-ordered scratch (hipMallocAsync) for its R2 filter.  Errors
+ * never throw across the ABI: every
  * call returns 0 on success or a negative KURA_E* code, and
  * kura_last_error() returns a thread-local message.
  *
@@ -22,6 +25,7 @@
  *   kura_reset           SpatialKuramoto.reset transient env.py:594-614
  *   kura_step            SpatialKuramoto.step            env.py:415-454
  *   kura_reward          reward_* on a given window      env.py:638-688
+ *   kura_reward_n        reward_* on any window length   env.py:638-688, utils.py:21-27
  *   kura_get/set_state   (no reference equivalent; env state was not
  *                        checkpointable)
  */
@@ -50,8 +54,13 @@ enum {
 /* per-env failure bits of a step/reset launch (kura_get_env_flags, and OR-ed
  * over the launch into kura_get_stats()[3]).  The reference's diffeqsolve
  * raises on a failed solve (diffrax throw=True, env.py:261-270); libkura never
- * throws: a failed env's step is abandoned (state not advanced, done = 1,
- * reward = 0, nsamp = 0, obs/lfp not written) and the host decides. */
+ * throws: a failed env's step is abandoned (done = 1, reward = 0, nsamp = 0,
+ * obs/lfp/window/time/step counter not written) and the host decides.  The
+ * env's phase state is then UNDEFINED -- if the stim-ON solve succeeded and
+ * the stim-OFF solve failed, y already holds the ON solve's last row (the
+ * oracle behaves the same way) -- so a failed env must be reset
+ * (KuraVectorEnv does this for on_failure="reset"); a failed reset likewise
+ * leaves t at the end of the transient with an undefined y. */
 enum {
     KURA_F_MAX_STEPS = 1,   /* diffeqsolve max_steps reached */
     KURA_F_NONFINITE = 2,   /* NaN/Inf state or RHS (non-finite error norm) */
@@ -173,12 +182,27 @@ int kura_step(KuraHandle* h, const float* action /* B*n_elec in [-1,1] */,
  * directly by aDBS_RL/agents/simple_dbs.py:83-90). */
 int kura_reward(KuraHandle* h, int kind, const double* window /* n*W device */, const float* u0 /* n device */,
                 double* reward /* n device */, int n, void* stream);
+/* the same on 1-D windows of ANY length len (row stride ld >= len, device):
+ * the reference's reward_* take the beta bins from len(x_state)
+ * (env.py:638-688 -> utils.py:21-27; e.g. PIDController.predict passes
+ * observation.ravel(), n_envs*W samples, aDBS_RL/agents/simple_dbs.py:81-88).
+ * cos_tab/sin_tab: n_bins rows of len twiddles cos/sin(2 pi k i / len) for
+ * the in-band bins k (device; unused for KURA_R_TEMP_CONST, which requires
+ * len > padlen as scipy.signal.filtfilt does).  A call with len == W and the
+ * handle's tables equals kura_reward bit for bit. */
+int kura_reward_n(KuraHandle* h, int kind, const double* x /* n*ld device */, int64_t len, int64_t ld, int n,
+                  const double* cos_tab, const double* sin_tab, int n_bins, const float* u0 /* n device */,
+                  double* reward /* n device */, void* stream);
 
 /* state snapshot for checkpoint/resume and parity tests (host pointers; syncs) */
 int kura_get_state(KuraHandle* h, float* y /* B*N */, double* t /* B */, int32_t* step /* B */,
                    double* ring /* B*W */, int32_t* wpos /* B */);
 int kura_set_state(KuraHandle* h, const float* y, const double* t, const int32_t* step,
                    const double* ring, const int32_t* wpos);
+/* diagnostic: copy the solver workspace (records, [B_pad/16][14][N][16]
+ * float32, B_pad = B rounded up to 16; syncs) to the host -- used to compare
+ * kernel generations record by record (tools/record_probe.py) */
+int kura_debug_read_workspace(KuraHandle* h, float* out, int64_t n);
 /* optional capture of every saved phase row of each kura_step: rows_dev
  * (device, B*(KURA_S_MAX+1)*N float32, or NULL to stop) receives, per env,
  * rows 0 .. S of the step -- ys_I then ys_II, the reference's sol_state_

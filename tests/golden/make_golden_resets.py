@@ -22,9 +22,10 @@ coordinates, the encapsulation coefficient and SHA-1 digests of w0 and theta0
 (float64 bytes) and the conductances (deduplicated arrays), for
   * env1 train (spatial variation every 10 resets) and env2 train, 40 resets
     of one env each;
-  * the evaluate_HF_DBS.py protocol (seed 228, five eval envs constructed in
-    order on the global RNG, then 1 + 5 resets per env, env by env) for
-    env0, env1 and env2."""
+  * the evaluate_HF_DBS.py protocol (seed 228; for each of the five eval
+    configs in turn generate_w0_with_locus then the constructor, all on the
+    global RNG; then 1 + 5 resets per env, env by env) for env0, env1 and
+    env2."""
 from __future__ import annotations
 
 import contextlib
@@ -130,20 +131,20 @@ def main(ref_root: str) -> None:
         put(tag, recs)
         print(tag, "encaps", out[f"{tag}_encaps"][:12], "elec moves", len(set(map(tuple, out[f"{tag}_elec"]))))
 
-    # (b) the evaluate_HF_DBS.py protocol: seed 228, 5 eval envs built in order, then 1 + 5 resets each
+    # (b) the evaluate_HF_DBS.py protocol: seed 228 (:20); for each of the 5 eval
+    # configs in turn generate_w0_with_locus then make_env (:195-218) -- the
+    # constructor reseeds the global RNG, so env k+1's frequencies follow env k's
+    # construction -- then 1 + 5 resets per env (evaluate_policy_)
     for tag, C in (("proto_env0", C0), ("proto_env1", C1), ("proto_env2", C2)):
         np.random.seed(228)
-        ds = []
-        for k in range(5):
-            d = copy.deepcopy(C.eval_envs_list[k])
-            d = fill(U, d)
-            d["reward_func"] = "bbpow_action"
-            d["dbs_action_bounds"] = [-5, 5]
-            ds.append(d)
         recs = []
         with quiet:
             envs = []
-            for d in ds:
+            for k in range(5):
+                d = copy.deepcopy(C.eval_envs_list[k])
+                d = fill(U, d)
+                d["reward_func"] = "bbpow_action"
+                d["dbs_action_bounds"] = [-5, 5]
                 envs.append(make_env(E, U, d))
                 recs.append(record(envs[-1]))
             for env in envs:

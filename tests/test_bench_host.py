@@ -33,10 +33,14 @@ def test_part_width_reaches_the_config():
             sim.make_config(p, 32, reward_func="bbpow_action", part_osc=bad)
 
 
-def test_bench_kernel_name():
+def test_bench_kernel_name(monkeypatch):
     bench = importlib.import_module("bench")
+    monkeypatch.delenv("KURA_KERNEL", raising=False)
+    assert bench.kernel_name(1024) == "kura_step1w_kernel<8, false>"     # K1w, one wave per SIMD
+    assert bench.kernel_name(512) == "kura_step1w_kernel<4, false>"
+    monkeypatch.setenv("KURA_KERNEL", "k1")                               # round-2 kernel (A/B)
     assert bench.kernel_name(1024) == "kura_step_kernel<4, false>"
-    assert bench.kernel_name(512) == "kura_step_kernel<2, false>"
+    monkeypatch.delenv("KURA_KERNEL")
     assert bench.kernel_name(8192) == "kura_step_kernel<4, true>"
     assert bench.kernel_name(8192, 256) == "kura_step_kernel<1, true>"
     assert bench.kernel_name(8192, 512) == "kura_step_kernel<2, true>"

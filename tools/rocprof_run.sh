@@ -12,7 +12,7 @@ O=$R/gpurun_out/${1:-prof}
 mkdir -p $O
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o run -- \
-    python3 $R/bench.py --steps 10 --warmup 2 --cpu-seconds 0 > $O/bench_trace.json 2> $O/trace.err
+    python3 $R/bench.py --steps 60 --warmup 3 --cpu-seconds 0 > $O/bench_trace.json 2> $O/trace.err
 timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/fetch -o run -- \
     python3 $R/bench.py --steps 3 --warmup 1 --cpu-seconds 0 > $O/bench_fetch.json 2> $O/fetch.err
 timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/write -o run -- \
