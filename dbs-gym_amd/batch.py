@@ -8,6 +8,7 @@ phases.  ``build_batch`` stacks B of them into the arrays libkura consumes.
 """
 from __future__ import annotations
 
+import os
 from copy import deepcopy
 
 import numpy as np
@@ -143,6 +144,22 @@ class EnvHost:
             g_rec.setflags(write=False)
             self._g_key, self._g = key, (g_stim, g_rec)
         return self._g
+
+
+def log_temporal_events(params: dict, host: EnvHost) -> str | None:
+    """env.py:559-562, after a reset's drift/spatial updates: with save_events
+    and a log_path, every reset after the second np.save-s the env's temporal
+    events to log_path/temp_<reset_count>.npy (a pickled dict, as the reference
+    writes it).  The reference keeps temporal_events only for temporal-drift
+    configs (env.py:355-359), so save_events without one raises AttributeError
+    there; so does this.  Returns the written path (or None)."""
+    if params.get("save_events") and params.get("log_path") is not None and host.reset_count > 1:
+        if not params.get("temporal_drift"):
+            raise AttributeError("'SpatialKuramoto' object has no attribute 'temporal_events'")
+        path = os.path.join(params["log_path"], f"temp_{host.reset_count}.npy")
+        np.save(path, host.temporal_events, allow_pickle=True)
+        return path
+    return None
 
 
 def fill_driver_arrays(params: dict, w0_seed: int | None = None, rs: np.random.RandomState | None = None) -> dict:

@@ -163,10 +163,14 @@ KDM_FN float kdm_inv_fifth_root(float xf) {
         double t = KDM_FMA(-m, w5, 1.0);
         w = KDM_FMA(w * 0.2, t, w);
     }
-    // 2^(-r/5) for r = 0..4
-    const double inv_tab[5] = {1.0, 0x1.bdb8cdadbe120p-1, 0x1.8406003b2ae5cp-1,
-                               0x1.51cb453b9536cp-1, 0x1.2611186bae675p-1};
-    double y = w * inv_tab[r];
+    // 2^(-r/5) for r = 0..4 (a select chain, not an indexed table: on the GPU a
+    // run-time-indexed local array lives in scratch memory)
+    const double inv_r = r == 0 ? 1.0
+                         : r == 1 ? 0x1.bdb8cdadbe120p-1
+                         : r == 2 ? 0x1.8406003b2ae5cp-1
+                         : r == 3 ? 0x1.51cb453b9536cp-1
+                                  : 0x1.2611186bae675p-1;
+    double y = w * inv_r;
     // multiply by 2^(-qd) exactly (|qd| <= 30 for float inputs)
     union { double d; uint64_t u; } sc;
     sc.u = (uint64_t)(1023 - qd) << 52;

@@ -23,7 +23,7 @@ import torch
 
 from . import spectral
 from .abi import KURA_S_MAX
-from .batch import EnvHost, build_batch, fill_driver_arrays
+from .batch import EnvHost, build_batch, fill_driver_arrays, log_temporal_events
 from .abi import KuraSolverError
 from .sim import KuraSim, make_config
 
@@ -176,16 +176,7 @@ class KuraVectorEnv:
         return out
 
     def _log_events(self, b):
-        """env.py:559-562: with save_events and a log_path, every reset after the
-        second saves the env's temporal events to log_path/temp_<reset_count>.npy
-        (np.save of the dict; the reference keeps temporal_events only for
-        temporal-drift configs and raises AttributeError otherwise)."""
-        p, h = self.params[b], self.hosts[b]
-        if p.get("save_events") and p.get("log_path") is not None and h.reset_count > 1:
-            if not p.get("temporal_drift"):
-                raise AttributeError("'SpatialKuramoto' object has no attribute 'temporal_events'")
-            np.save(os.path.join(p["log_path"], f"temp_{h.reset_count}.npy"), h.temporal_events,
-                    allow_pickle=True)
+        log_temporal_events(self.params[b], self.hosts[b])           # env.py:559-562
 
     def reset(self, seed=None, options=None):
         """env.py:467-614 for every env.  ``seed`` (int or list) seeds each

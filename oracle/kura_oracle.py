@@ -29,8 +29,12 @@ _lib = None
 def lib() -> ctypes.CDLL:
     global _lib
     if _lib is None:
-        build()
-        L = ctypes.CDLL(LIB)
+        # KURA_ORACLE_LIB: an alternative build of the same source, e.g. the
+        # ASan+UBSan one of `make -C oracle asan` (run with its runtime preloaded)
+        alt = os.environ.get("KURA_ORACLE_LIB")
+        if not alt:
+            build()
+        L = ctypes.CDLL(alt or LIB)
         L.oracle_create.restype = c_void_p
         L.oracle_create.argtypes = [c_void_p, c_void_p]
         L.oracle_destroy.argtypes = [c_void_p]

@@ -67,9 +67,10 @@ def test_env2_n1024_vector_env(torch_gpu):
     env.close()
 
 
-@pytest.mark.parametrize("name,reward", [("env0", "bbpow_action"), ("env1", "temp_const_action")])
-def test_full_grid_b4096_sampled(torch_gpu, name, reward):
-    """configs[1]/[2] at full size: B=4096 (256 workgroups), reset + 3 steps;
+@pytest.mark.parametrize("name,reward,steps", [("env0", "bbpow_action", 50), ("env1", "temp_const_action", 50),
+                                               ("env1", "bbpow_action", 50)])
+def test_full_grid_b4096_sampled(torch_gpu, name, reward, steps):
+    """configs[1]/[2] at full size: B=4096 (256 workgroups), reset + 50 steps;
     envs sampled from first, middle and last workgroups and across the
     16-env interleave checked bit for bit against the oracle run on just them."""
     torch = torch_gpu
@@ -90,7 +91,7 @@ def test_full_grid_b4096_sampled(torch_gpu, name, reward):
     o.set_spectral(ct, st)
     o.reset(th0[idx])
     _cmp_state({k: v[idx] for k, v in sim.get_state().items()}, o.state(), "reset")
-    for k in range(3):
+    for k in range(steps):
         a = actions("rand", B, cfg.n_elec, k)
         sim.step(torch.from_numpy(a), check_errors=True)
         ref = o.step(a[idx])
@@ -120,3 +121,68 @@ def test_largest_window_parity(torch_gpu):
     limit (WPL_MAX = 40 samples per lane), R1 and the window ring at its largest."""
     g, o = _run_pair(torch_gpu, "env0", 256, 19, "bbpow_action", 6, "rand", observe_wind_counts=142)
     np.testing.assert_array_equal(g["ring"], o["ring"])
+
+
+def test_r3_n1024_parity(torch_gpu):
+    """R3 (reward_bbpow_threth_action) at the headline N=1024 (VERDICT r02 weak #8)."""
+    g, o = _run_pair(torch_gpu, "env0", 1024, 19, "bbpow_threth_action", 8, "rand")
+    np.testing.assert_array_equal(g["y"], o["y"])
+
+
+def test_env2_b4096_vector_env_sampled(torch_gpu):
+    """configs[3] per GPU at full size (VERDICT r02 weak #8): env2 (drift,
+    per-env K ~ U(0.3, 0.8)) at N=1024 x 4096 envs through KuraVectorEnv with
+    masked autoreset across an episode boundary (episode of 3 steps, 5 steps
+    run); 12 envs sampled across the grid checked bit for bit against the
+    oracle run on just them, their reset draws replayed by fresh EnvHosts."""
+    vec = importlib.import_module("dbs-gym_amd.vec_env")
+    import copy
+    B, N = 4096, 1024
+    base = kura.fill_driver_arrays(kura.synthetic_params("env2", N), w0_seed=31)
+    Ks = np.random.default_rng(9).uniform(0.3, 0.8, B)
+    plist = []
+    for b in range(B):
+        p = copy.copy(base)
+        p["K"] = float(Ks[b])
+        p["rand_seed"] = 1000 + b
+        plist.append(p)
+    env = vec.KuraVectorEnv(plist, reward_func="bbpow_action")
+    env.episode_steps = 3
+    idx = np.array([0, 5, 15, 16, 255, 1024, 2047, 2049, 3000, 4079, 4088, 4095])
+    sub = [plist[i] for i in idx]
+    c = copy.copy(env.cfg)
+    c.n_envs = len(idx)
+    o = ko.Oracle(c, env._alpha.astype(np.float32))
+    o.set_gain(np.array([np.float32(p["K"] / N) for p in sub], np.float32))
+    bins = kura.spectral.beta_bins(c.window, base["verbose_dt"])
+    o.set_spectral(*kura.spectral.twiddles(c.window, bins))
+    hosts = [kura.EnvHost(p) for p in sub]
+    n = len(idx)
+    ne, nr = c.n_elec, max(c.n_rec, 1)
+    st = dict(w=np.zeros((n, N)), gs=np.zeros((n, ne, N)), gr=np.zeros((n, nr, N)), th=np.zeros((n, N)))
+
+    def draw():
+        for j in range(n):
+            w0, gs, gr, th = hosts[j].reset_draws()
+            st["w"][j], st["gs"][j], st["gr"][j], st["th"][j] = w0, gs, gr, th
+        o.set_env_params(st["w"].astype(np.float32), st["gs"], st["gr"])
+
+    obs, _ = env.reset()
+    draw()
+    np.testing.assert_array_equal(obs[idx, 0].cpu().numpy(), o.reset(st["th"].astype(np.float32)))
+    rng = np.random.default_rng(3)
+    for k in range(5):
+        a = rng.uniform(-1, 1, (B, ne)).astype(np.float32)
+        obs, rew, term, trunc, info = env.step(a)
+        ref = o.step(a[idx])
+        np.testing.assert_array_equal(rew.cpu().numpy()[idx], ref["reward"], err_msg=f"reward step {k}")
+        np.testing.assert_array_equal(env.sim.lfp_true.cpu().numpy()[idx], ref["lfp_true"])
+        if (k + 1) % 3 == 0:
+            assert len(info["terminal_env_ids"]) == B
+            np.testing.assert_array_equal(info["terminal_observation"][idx, 0].cpu().numpy(), ref["obs"])
+            draw()
+            np.testing.assert_array_equal(obs[idx, 0].cpu().numpy(), o.reset(st["th"].astype(np.float32)))
+        else:
+            np.testing.assert_array_equal(obs[idx, 0].cpu().numpy(), ref["obs"])
+    np.testing.assert_array_equal(env.sim.get_state()["y"][idx], o.state()["y"])
+    env.close()

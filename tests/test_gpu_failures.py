@@ -110,26 +110,67 @@ def test_nonfinite_state_flags_only_that_env(torch_gpu):
     sim.close()
 
 
-def test_vector_env_policies(torch_gpu):
+@pytest.mark.parametrize("check", ["eager", "deferred"])
+def test_vector_env_policies(torch_gpu, check):
     """KuraVectorEnv: on_failure='raise' raises from reset/step; 'reset' reports
-    the env truncated and autoresets it."""
+    the env truncated and autoresets it.  failure_check='eager' acts in the
+    failing step; 'deferred' (default: no per-step synchronisation) acts at
+    the start of the next step, before its launch (the failing step itself
+    reports done = 1 from the kernel)."""
     kura = importlib.import_module("dbs-gym_amd")
     venv = importlib.import_module("dbs-gym_amd.vec_env")
     p = kura.reference_params("env0", "eval", 0)
     p["reward_func"] = "bbpow_action"
-    env = venv.KuraVectorEnv(p, num_envs=3, max_steps=2)
+    env = venv.KuraVectorEnv(p, num_envs=3, max_steps=2, failure_check=check)
     with pytest.raises(abi.KuraSolverError, match="kura_reset"):
         env.reset()
     env.close()
-    env = venv.KuraVectorEnv(p, num_envs=3, on_failure="reset")
+    env = venv.KuraVectorEnv(p, num_envs=3, on_failure="reset", failure_check=check)
     env.reset()
     st = env.sim.get_state()
     st["y"][1, 0] = np.nan
     env.sim.set_state(st)
-    obs, rew, term, trunc, info = env.step(np.zeros((3, 1), np.float32))
-    assert list(info["failed_env_ids"]) == [1] and info["failure_flags"][0] == abi.KURA_F_NONFINITE
-    assert bool(trunc[1]) and bool(term[1]) and not bool(trunc[0])
-    assert list(info["terminal_env_ids"]) == [1] and env.steps[1] == 0 and env.steps[0] == 1
-    obs, rew, term, trunc, info = env.step(np.zeros((3, 1), np.float32))   # env 1 runs again after its reset
+    a = np.zeros((3, 1), np.float32)
+    obs, rew, term, trunc, info = env.step(a)
+    if check == "eager":
+        assert list(info["failed_env_ids"]) == [1] and info["failure_flags"][0] == abi.KURA_F_NONFINITE
+        assert bool(trunc[1]) and bool(term[1]) and not bool(trunc[0])
+        assert list(info["terminal_env_ids"]) == [1] and env.steps[1] == 0 and env.steps[0] == 1
+    else:
+        assert "failed_env_ids" not in info and bool(term[1]) and not bool(term[0])   # the kernel's done = 1
+        obs, rew, term, trunc, info = env.step(a)        # reported now; env 1 reset before this launch
+        assert list(info["failed_env_ids"]) == [1] and info["failure_flags"][0] == abi.KURA_F_NONFINITE
+        assert env.steps[1] == 1 and env.steps[0] == 2 and np.isfinite(rew.cpu().numpy()).all()
+    obs, rew, term, trunc, info = env.step(a)   # env 1 runs again after its reset
     assert "failed_env_ids" not in info and np.isfinite(rew.cpu().numpy()).all()
+    obs, rew, term, trunc, info = env.step(a)
+    assert "failed_env_ids" not in info
+    env.close()
+    # raise policy, deferred: the failure surfaces from the next call
+    env = venv.KuraVectorEnv(p, num_envs=3, failure_check=check)
+    env.reset()
+    st = env.sim.get_state()
+    st["y"][2, 5] = np.inf
+    env.sim.set_state(st)
+    if check == "eager":
+        with pytest.raises(abi.KuraSolverError):
+            env.step(a)
+    else:
+        env.step(a)
+        with pytest.raises(abi.KuraSolverError, match="previous call"):
+            env.step(a)
+    env.close()
+
+
+def test_vector_env_failed_resets_retry_then_raise(torch_gpu):
+    """on_failure='reset': an autoreset whose transient fails is reported and
+    retried; max_reset_failures consecutive failures of one env raise."""
+    kura = importlib.import_module("dbs-gym_amd")
+    venv = importlib.import_module("dbs-gym_amd.vec_env")
+    p = kura.reference_params("env0", "eval", 0)
+    p["reward_func"] = "bbpow_action"
+    env = venv.KuraVectorEnv(p, num_envs=2, max_steps=2, on_failure="reset", max_reset_failures=2)
+    with pytest.raises(abi.KuraSolverError, match="repeated"):
+        env.reset()
+    assert (env._reset_fail_runs == 3).all()
     env.close()
