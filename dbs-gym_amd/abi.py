@@ -133,7 +133,7 @@ def load_library(path: str | None = None) -> ctypes.CDLL:
     global _lib
     if _lib is not None and path is None:
         return _lib
-    p = path or LIB_PATH
+    p = path or os.environ.get("KURA_LIB") or LIB_PATH  # KURA_LIB: an alternative build (A/B diagnostics)
     if not os.path.exists(p):
         raise RuntimeError(
             f"libkura.so not found at {p}: build it with `python -c 'import __graft_entry__ as g; g.build()'` "

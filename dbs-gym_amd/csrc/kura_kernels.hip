@@ -113,7 +113,7 @@ struct DevParams {
 // Diagnostic phase timers (compile with -DKURA_STAMPS): per wave, cycles
 // spent in each phase (tools/phase_stamps.py names them), accumulated with
 // s_memtime and added into p.stamps[wave][KURA_NSTAMP] at the end.
-#define KURA_NSTAMP 20
+#define KURA_NSTAMP 24
 #ifdef KURA_STAMPS
 #define STAMP_DECL unsigned long long st_acc[KURA_NSTAMP] = {}; unsigned long long st_last = __builtin_amdgcn_s_memtime();
 #define STAMP(k) do { unsigned long long n_ = __builtin_amdgcn_s_memtime(); st_acc[k] += n_ - st_last; st_last = n_; } while (0)
@@ -1287,6 +1287,8 @@ __device__ void solve_wg(const DevParams& __restrict__ p, float* Xs, int env_bas
     *rhs_count += nrhs;
 }
 
+#include "kura_k1t.inc"
+
 __device__ __forceinline__ void flush_stats(const DevParams& p, long long rhs, int env_base) {
     if (threadIdx.x != 0) return;
     unsigned long long steps = 0, rej = 0, flags = 0;
@@ -1338,7 +1340,7 @@ struct WinView {
     const double* ring;
     int e;
     int W, wp0, S;
-    __device__ double at(int i) const {
+    __device__ __forceinline__ double at(int i) const {
         const int keep = W - S;
         if (i < keep) {
             int k = wp0 + S + i;
@@ -1478,6 +1480,85 @@ __device__ __forceinline__ double reward_of(const DevParams& p, const double (&x
 
 #define WPL_MAX 40  // ceil(W/64) upper bound supported (W <= 2560)
 
+// Beta-band power (calc_beta_band_power's sum over the bins, utils.py:21-27)
+// of the windows of NE envs of one wave at once, in the R64 order of
+// window_dot: lane l accumulates x[l + 64 m] * tab[l + 64 m] over m from +0,
+// then the xor butterfly; bins are added in index order from +0.  The bins
+// go in groups of BG (accumulators in registers); within a group every
+// twiddle element is loaded once for all NE envs (buffer loads through one
+// wave-uniform descriptor, 4 columns in flight), and the windows are read
+// straight from the ring / this step's samples (WinView).  ok[e] false:
+// bb[e] = 0 and nothing of env e is read.
+#define BB_G 5
+template <int NE>
+__device__ __forceinline__ void bbpow_multi(const DevParams& __restrict__ p, const WinView (&xv)[NE],
+                                            const bool (&ok)[NE], double (&bb)[NE]) {
+    const int lane = threadIdx.x & 63;
+    const int W = p.W, nb = p.n_bins;
+    const int nm = (W + 63) / 64;
+    const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc((void*)uniform_ptr(p.ctab), 0, nb * W * 8,
+                                                                      0x00020000);
+    const __amdgpu_buffer_rsrc_t rsn = __builtin_amdgcn_make_buffer_rsrc((void*)uniform_ptr(p.stab), 0, nb * W * 8,
+                                                                       0x00020000);
+    auto ld = [&](const __amdgpu_buffer_rsrc_t& r, int off) {
+        return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
+    };
+#pragma unroll
+    for (int e = 0; e < NE; ++e) bb[e] = 0.0;
+#pragma unroll 1
+    for (int b0 = 0; b0 < nb; b0 += BB_G) {
+        double re[NE][BB_G], im[NE][BB_G];
+#pragma unroll
+        for (int e = 0; e < NE; ++e)
+#pragma unroll
+            for (int g = 0; g < BB_G; ++g) re[e][g] = im[e][g] = 0.0;
+#pragma unroll 4
+        for (int m = 0; m < nm; ++m) {
+            const int i = lane + 64 * m;
+            const bool valid = i < W;
+            double x[NE];
+#pragma unroll
+            for (int e = 0; e < NE; ++e) x[e] = (valid && ok[e]) ? xv[e].at(i) : 0.0;
+#pragma unroll
+            for (int g = 0; g < BB_G; ++g) {
+                if (b0 + g >= nb) break;  // wave-uniform
+                const int off = valid ? ((b0 + g) * W + i) * 8 : 0x7FFFFFF0;  // out of range: 0, unused
+                const double c = ld(rc, off), sn = ld(rsn, off);
+#pragma unroll
+                for (int e = 0; e < NE; ++e) {
+                    re[e][g] = valid ? __builtin_fma(x[e], c, re[e][g]) : re[e][g];
+                    im[e][g] = valid ? __builtin_fma(x[e], sn, im[e][g]) : im[e][g];
+                }
+            }
+        }
+#pragma unroll
+        for (int g = 0; g < BB_G; ++g) {
+            if (b0 + g >= nb) break;
+#pragma unroll
+            for (int e = 0; e < NE; ++e) {
+                const double pr = wave_sum_f64(re[e][g]) / (double)W, pi = wave_sum_f64(im[e][g]) / (double)W;
+                bb[e] = bb[e] + (pr * pr + pi * pi) * 2.0;
+            }
+        }
+    }
+}
+// reward_of's closing expressions (env.py:638-688) from the band power bb (R1,
+// R3) or the filter term d (R2)
+__device__ __forceinline__ double reward_from(const DevParams& p, double bb, double d, double u0) {
+    const double au = fabs(u0);
+    if (p.reward_kind == KURA_R_TEMP_CONST) {
+        const double r1 = 1e3 * (d * d);
+        return -r1 - 1e-2 * au;
+    }
+    if (p.reward_kind == KURA_R_BBPOW_THR) {
+        const double bs = 1e4 * bb;
+        const double r1 = bs > 20.0 ? 5.0 : 0.0;
+        return -r1 - au;
+    }
+    const double r1 = 1e4 * bb;
+    return -r1 - 1e-2 * au;
+}
+
 // ------------------------------------------------------------ step kernel --
 // Work item of a launch: (env group, part).  For N <= 1024 one workgroup per
 // group; split groups loop persistently over pairs with a grid that is a
@@ -1594,13 +1675,21 @@ __device__ void r2_filters_wg(const DevParams& p, int env_base, double (&out)[EN
 // Launch-wide failure bits an env inherits: a split-group barrier that timed
 // out (group_barrier) leaves every later exchange of the launch unsynchronised.
 __device__ __forceinline__ int launch_flags(const DevParams& p, bool xl) {
-    if (!xl) return 0;
+    if (!xl) return 0;  // (xl: split groups, or K1t's team waits -- both can time out)
     const unsigned long long v = __hip_atomic_load((__attribute__((address_space(1))) unsigned long long*)&p.stats[3],
                                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return (int)(v & KURA_F_BARRIER);
 }
 
-template <int TPW, bool XL>
+// the workgroup solver of a step / reset: K1's solve_wg, or K1t's solve_t (TEAM)
+template <int TPW, bool XL, bool TEAM>
+__device__ __forceinline__ void solve_sel(const DevParams& __restrict__ p, float* Xs, int env_base, bool to_ring,
+                                          bool pulse_on, long long* rhs, Part& pt) {
+    if constexpr (TEAM) solve_t<TPW>(p, Xs, env_base, to_ring, pulse_on, rhs, pt);
+    else solve_wg<TPW, XL>(p, Xs, env_base, to_ring, pulse_on, rhs, pt);
+}
+
+template <int TPW, bool XL, bool TEAM = false>
 __device__ __forceinline__ void step_pair(const DevParams& p, Part& pt, float* Xs, const float* __restrict__ action,
                                           float* __restrict__ obs, double* __restrict__ reward,
                                           uint8_t* __restrict__ done, float* __restrict__ lfp_true,
@@ -1654,7 +1743,7 @@ __device__ __forceinline__ void step_pair(const DevParams& p, Part& pt, float* X
     }
     __syncthreads();
     long long rhs = 0;
-    solve_wg<TPW, XL>(p, Xs, env_base, false, true, &rhs, pt);
+    solve_sel<TPW, XL, TEAM>(p, Xs, env_base, false, true, &rhs, pt);
     __syncthreads();  // global stores of the solve (y) before the OFF setup
     // ---- stimulation OFF (env.py:433-441)
     if (tid < E_WG) {
@@ -1677,17 +1766,34 @@ __device__ __forceinline__ void step_pair(const DevParams& p, Part& pt, float* X
         }
     }
     __syncthreads();
-    solve_wg<TPW, XL>(p, Xs, env_base, false, false, &rhs, pt);
+    solve_sel<TPW, XL, TEAM>(p, Xs, env_base, false, false, &rhs, pt);
+    STAMP_DECL  // diagnostic build: the tail's phases in slots 20-22
     __syncthreads();
     // ---- window, reward, outputs (env.py:443-454): wave w owns envs 2w, 2w+1
     // (split groups: part 0; every part holds the same samples)
-    constexpr int WPL = WPL_MAX;
     // R2: the serial filters of all 16 envs of the workgroup run in one wave,
     // one lane per env (r2_filters_wg), before the per-env loop (and so before
     // the ring appends)
     double r2d[ENVS_PER_WAVE] = {0.0, 0.0};
     const bool r2 = p.reward_kind == KURA_R_TEMP_CONST && (!XL || pt.part == 0);
     if (r2) r2_filters_wg(p, env_base, r2d);
+    // R1 / R3: beta-band power of both envs of the wave at once, before the
+    // ring appends below overwrite the window's oldest slots
+    double bbv[ENVS_PER_WAVE] = {0.0, 0.0};
+    if (!r2 && (!XL || pt.part == 0)) {
+        WinView xvs[ENVS_PER_WAVE];
+        bool oks[ENVS_PER_WAVE];
+#pragma unroll
+        for (int ee = 0; ee < ENVS_PER_WAVE; ++ee) {
+            const int e = wave * ENVS_PER_WAVE + ee;
+            const int env = env_base + e;
+            const int S = s_nI[e] + s_nII[e] - 1;
+            oks[ee] = env < p.B && !(s_ctl[e].flags | launch_flags(p, XL || TEAM)) && S >= 1;
+            xvs[ee] = WinView{p.ring + (size_t)(oks[ee] ? env : 0) * p.W, e, p.W, oks[ee] ? p.wpos[env] : 0, S};
+        }
+        bbpow_multi<ENVS_PER_WAVE>(p, xvs, oks, bbv);
+    }
+    STAMP(21);
 #pragma unroll 1
     for (int ee = 0; ee < ((!XL || pt.part == 0) ? ENVS_PER_WAVE : 0); ++ee) {
         const int e = wave * ENVS_PER_WAVE + ee;
@@ -1695,7 +1801,7 @@ __device__ __forceinline__ void step_pair(const DevParams& p, Part& pt, float* X
         if (env >= p.B) continue;
         const CtlE& c = s_ctl[e];
         const int S = s_nI[e] + s_nII[e] - 1;
-        const int fl = c.flags | launch_flags(p, XL);
+        const int fl = c.flags | launch_flags(p, XL || TEAM);
         if (lane == 0) p.eflags[env] = fl;
         if (fl || S < 1) {
             // failed step (kura.h KURA_F_*): no state advance, done = 1; the
@@ -1711,19 +1817,14 @@ __device__ __forceinline__ void step_pair(const DevParams& p, Part& pt, float* X
         double* rb = p.ring + (size_t)env * W;
         const int wp0 = p.wpos[env];
         const WinView xv{rb, e, W, wp0, S};
-        double x[WPL];
-#pragma unroll
-        for (int m = 0; m < WPL; ++m) {
-            const int i = lane + 64 * m;
-            x[m] = 0.0;
-            if (i < W) {
-                x[m] = xv.at(i);
-                if (obs) obs[(size_t)env * W + i] = (float)x[m];
-            }
-        }
-        double* ext = p.scratch + (size_t)env * 2 * (W + 2 * p.padlen);
-        double* tmp = ext + (W + 2 * p.padlen);
-        const double r = reward_of<WPL, true>(p, x, s_u[e][0], xv, ext, tmp, &r2d[ee]);
+        STAMP(22);
+        if (obs)
+            for (int i = lane; i < W; i += 64) obs[(size_t)env * W + i] = (float)xv.at(i);
+#ifdef KURA_STAMPS
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+        STAMP(20);
+        const double r = reward_from(p, bbv[ee], r2d[ee], s_u[e][0]);
         // ring append after every read of the old slots
         if (lane < S) {
             int k = wp0 + lane;
@@ -1752,6 +1853,8 @@ __device__ __forceinline__ void step_pair(const DevParams& p, Part& pt, float* X
             if (lane == 0) p.ep_len[env] = L0 + S;
         }
     }
+    STAMP(22);
+    STAMP_FLUSH(p);
     if (!XL || pt.part == 0) flush_stats(p, rhs, env_base);
 }
 
@@ -1788,7 +1891,7 @@ __global__ __launch_bounds__(NTHREADS) void kura_step_kernel(DevParams p, const 
 }
 
 // ----------------------------------------------------------- reset kernel --
-template <int TPW, bool XL>
+template <int TPW, bool XL, bool TEAM = false>
 __device__ __forceinline__ void reset_pair(const DevParams& p, Part& pt, float* Xs, const uint8_t* __restrict__ mask,
                                            const float* __restrict__ theta0, float* __restrict__ obs) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, tid = threadIdx.x;
@@ -1813,7 +1916,7 @@ __device__ __forceinline__ void reset_pair(const DevParams& p, Part& pt, float* 
     }
     __syncthreads();
     long long rhs = 0;
-    solve_wg<TPW, XL>(p, Xs, env_base, true, false, &rhs, pt);
+    solve_sel<TPW, XL, TEAM>(p, Xs, env_base, true, false, &rhs, pt);
     __syncthreads();  // ring rows written by thread e are read by every lane below
 #pragma unroll 1
     for (int ee = 0; ee < ((!XL || pt.part == 0) ? ENVS_PER_WAVE : 0); ++ee) {
@@ -1821,7 +1924,7 @@ __device__ __forceinline__ void reset_pair(const DevParams& p, Part& pt, float* 
         const int env = env_base + e;
         if (env >= p.B || (mask && !mask[env])) continue;
         if (lane == 0) {
-            p.eflags[env] = s_ctl[e].flags | launch_flags(p, XL);
+            p.eflags[env] = s_ctl[e].flags | launch_flags(p, XL || TEAM);
             p.t[env] = grid_at_c(s_ctl[e], s_ctl[e].n - 1);
             p.step[env] = 0;
             p.wpos[env] = 0;
@@ -1848,6 +1951,25 @@ __global__ __launch_bounds__(NTHREADS) void kura_reset_kernel(DevParams p, const
         Part pt = make_part(p, blockIdx.x);
         reset_pair<TPW, XL>(p, pt, Xs, mask, theta0, obs);
     }
+}
+
+// K1t / K2t (kura_k1t.inc): K1's step / reset with the team-overlapped solver
+template <int TPW>
+__global__ __launch_bounds__(NTHREADS) void kura_stept_kernel(DevParams p, const float* __restrict__ action,
+                                                              float* __restrict__ obs, double* __restrict__ reward,
+                                                              uint8_t* __restrict__ done, float* __restrict__ lfp_true,
+                                                              double* __restrict__ lfp_rec, int* __restrict__ nsamp) {
+    extern __shared__ float Xs[];
+    Part pt = make_part(p, blockIdx.x);
+    step_pair<TPW, false, true>(p, pt, Xs, action, obs, reward, done, lfp_true, lfp_rec, nsamp);
+}
+template <int TPW>
+__global__ __launch_bounds__(NTHREADS) void kura_resett_kernel(DevParams p, const uint8_t* __restrict__ mask,
+                                                               const float* __restrict__ theta0,
+                                                               float* __restrict__ obs) {
+    extern __shared__ float Xs[];
+    Part pt = make_part(p, blockIdx.x);
+    reset_pair<TPW, false, true>(p, pt, Xs, mask, theta0, obs);
 }
 
 // ------------------------------------------------------ standalone reward --
@@ -1883,14 +2005,14 @@ __global__ __launch_bounds__(64) void kura_reward_kernel(DevParams p, const doub
 __global__ __launch_bounds__(64) void kura_reward_n_kernel(DevParams p, const double* __restrict__ x, long long ld,
                                                            const double* __restrict__ ctab,
                                                            const double* __restrict__ stab, int n_bins,
-                                                           const float* __restrict__ u0, double* __restrict__ out,
+                                                           const double* __restrict__ u0, double* __restrict__ out,
                                                            double* __restrict__ scratch, int n) {
     const int j = blockIdx.x;
     if (j >= n) return;
     const int lane = threadIdx.x;
     const int L = p.W;
     const double* xw = x + (size_t)j * ld;
-    const double au = fabs((double)u0[j]);
+    const double au = fabs(u0[j]);  // float64: the caller's action as given (env.py:638-688)
     double r;
     if (p.reward_kind == KURA_R_TEMP_CONST) {
         const WinView v1[1] = {WinView{xw, 0, L, 0, 0}};

@@ -290,7 +290,7 @@ class KuraSim:
         """reward_* of n windows of any length L (x: (n, L)); twiddles (n_bins, L)
         for that length (kura_reward_n)."""
         w = x.to(self.device, torch.float64).contiguous()
-        u = u0.to(self.device, torch.float32).contiguous()
+        u = u0.to(self.device, torch.float64).contiguous()
         n, L = w.shape
         ct = torch.as_tensor(np.ascontiguousarray(cos_tab, np.float64), device=self.device)
         st = torch.as_tensor(np.ascontiguousarray(sin_tab, np.float64), device=self.device)
@@ -315,7 +315,7 @@ class KuraSim:
         return out
 
     def stamps(self) -> np.ndarray:
-        out = np.zeros((8, 20), np.uint64)   # [wave][KURA_NSTAMP]
+        out = np.zeros((8, 24), np.uint64)   # [wave][KURA_NSTAMP]
         check(self.lib, self.lib.kura_get_stamps(self._h, out.ctypes.data), "kura_get_stamps")
         return out
 

@@ -460,10 +460,10 @@ class KuraVectorEnv:
         as in the reference (utils.py:21-27)."""
         w = torch.as_tensor(np.asarray(windows, np.float64), device=self.device)
         w = w.reshape(1, -1) if w.ndim == 1 else w.reshape(w.shape[0], -1)
-        u = torch.as_tensor(np.asarray(u0, np.float32), device=self.device).reshape(-1)
+        # the action as the caller gives it, in float64 (the step kernels take
+        # the float32 actions of the action space, env.py:310-312)
+        u = torch.as_tensor(np.asarray(u0, np.float64), device=self.device).reshape(-1)
         L = int(w.shape[1])
-        if L == self.W:
-            return self.sim.reward_of(w, u, kind)
         kind = kind or self.cfg.reward_kind
         bins = spectral.beta_bins(L, self.params[0]["verbose_dt"])
         ct, st = spectral.twiddles(L, bins) if len(bins) else (np.zeros((0, L)), np.zeros((0, L)))

@@ -191,7 +191,7 @@ int kura_reward(KuraHandle* h, int kind, const double* window /* n*W device */, 
  * len > padlen as scipy.signal.filtfilt does).  A call with len == W and the
  * handle's tables equals kura_reward bit for bit. */
 int kura_reward_n(KuraHandle* h, int kind, const double* x /* n*ld device */, int64_t len, int64_t ld, int n,
-                  const double* cos_tab, const double* sin_tab, int n_bins, const float* u0 /* n device */,
+                  const double* cos_tab, const double* sin_tab, int n_bins, const double* u0 /* n device, float64 */,
                   double* reward /* n device */, void* stream);
 
 /* state snapshot for checkpoint/resume and parity tests (host pointers; syncs) */

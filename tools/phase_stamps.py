@@ -1,5 +1,8 @@
 #!/usr/bin/env python3
-"""Diagnostic: per-phase cycle breakdown of kura_step_kernel (KURA_STAMPS build).
+"""Diagnostic: per-phase cycle breakdown of the step kernel (KURA_STAMPS build;
+KURA_KERNEL=k1t (default) | k1 | k1w selects the kernel; K1t reuses K1's phase
+slots: gemm = both GEMM halves, barrier1 = the team waits before them,
+barrier2 = the pass's WAR wait or the step-end barrier; slot 19 = 1 + SIMD id).
 
 Builds dbs-gym_amd/csrc/libkura_stamps.so with -DKURA_STAMPS and runs a few
 bench-shaped steps, printing the share of wave cycles in each phase."""
@@ -15,9 +18,16 @@ import __graft_entry__ as ge  # noqa: E402
 
 SI = os.environ.get("SI") == "1"  # stage-input sub-phases (KURA_STAMPS_SI build, no record prefetch)
 LIB = os.path.join(ge.CSRC, "libkura_stamps_si.so" if SI else "libkura_stamps.so")
+KERN = os.environ.get("KURA_KERNEL", "k1")
+K1W = KERN == "k1w"
+# K1w (kura_k1w.inc) reuses the slots with its own phase names
+PHASES_W1 = ["stage_pass", "barrier_pre_gemm", "gemm", "-", "barrier_post_gemm", "last_pass", "err_barrier",
+             "decide", "saves", "fsal", "outside_solve", "reward_tail", "-", "-", "-", "-", "-", "-", "-", "-",
+             "-", "-", "-", "-"]
 PHASES = ["stage_input", "barrier1", "gemm", "epilogue", "barrier2", "post_err", "flag_sync", "post_decide",
           "post_saves", "post_fsal", "post_time", "save_setup", "save_loadwait", "save_compute", "save_publish",
-          "save_totals", "si_load", "si_compute", "si_lds", "si_misc"]
+          "save_totals", "si_load", "si_compute", "si_lds", "si_misc", "tail_window", "tail_reward", "tail_other",
+          "simd_id"]
 
 
 def main():
@@ -63,15 +73,18 @@ def main():
         ev_ms = ms_reset
     else:
         ev_ms = ev0.elapsed_time(ev1) / nsteps
+    names = PHASES_W1 if K1W else PHASES
+    nwaves = 4 if K1W else 8
+    s = s[:nwaves]
     tot = s.sum(axis=1, keepdims=True)
     share = (s / np.maximum(tot, 1)).mean(axis=0)
     nwg = (cfg.n_envs + 15) // 16
-    cyc_per_step_wave = s.sum(axis=0) / (8 * nwg * nsteps)
+    cyc_per_step_wave = s.sum(axis=0) / (nwaves * nwg * nsteps)
     out = {"mode": os.environ.get("MODE", "step"), "ms_per_launch": ev_ms,
-           "share": dict(zip(PHASES, [round(float(x), 4) for x in share])),
-           "cycles_per_step_per_wave": dict(zip(PHASES, [round(float(x)) for x in cyc_per_step_wave])),
+           "kernel": KERN, "share": dict(zip(names, [round(float(x), 4) for x in share])),
+           "cycles_per_step_per_wave": dict(zip(names, [round(float(x)) for x in cyc_per_step_wave])),
            # per wave (rows), cycles per step of the phases that differ between waves
-           "per_wave": {PHASES[k]: [round(float(v)) for v in s[:, k] / (nwg * nsteps)]
+           "per_wave": {names[k]: [round(float(v)) for v in s[:, k] / (nwg * nsteps)]
                         for k in range(len(PHASES)) if s[:, k].sum() > 0}}
     print(json.dumps(out))
 
