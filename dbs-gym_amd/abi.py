@@ -21,11 +21,13 @@ KURA_F_MAX_STEPS = 1
 KURA_F_NONFINITE = 2
 KURA_F_GRID = 8
 KURA_F_BARRIER = 16
+KURA_F_BOUNDS = 32     # KURA_DEBUG builds only
 FLAG_NAMES = {
     KURA_F_MAX_STEPS: "The maximum number of solver steps was reached",   # diffrax's message (throw=True)
     KURA_F_NONFINITE: "non-finite (NaN/Inf) state or RHS",
     KURA_F_GRID: "save grid outside [2, KURA_S_MAX] samples",
-    KURA_F_BARRIER: "split-group barrier timed out",
+    KURA_F_BARRIER: "split-group barrier (or K1t team wait) timed out",
+    KURA_F_BOUNDS: "device access outside its buffer (KURA_DEBUG build)",
 }
 
 KURA_REC_NAIVE = 0

@@ -128,6 +128,20 @@ struct DevParams {
 #define STAMP_ARGS
 #endif
 
+// Debug build (-DKURA_DEBUG, libkura_debug.so): every record, alpha, ring and
+// LFP-sample access is checked against the extent of its buffer; a violation
+// raises KURA_F_BOUNDS in kura_get_stats()[3] (and the per-env flags of the
+// envs the launch finishes), so a raw buffer access that the hardware range
+// check would silently turn into a zero read or a dropped store is named.
+#ifdef KURA_DEBUG
+#define KDBG_CHECK(stats, ok)                                                                     \
+    do {                                                                                          \
+        if ((stats) && !(ok)) atomicOr((stats) + 3, (unsigned long long)KURA_F_BOUNDS);           \
+    } while (0)
+#else
+#define KDBG_CHECK(stats, ok) do { } while (0)
+#endif
+
 // Per-workgroup LDS besides the dynamic 32 x N operand: LFP samples of the
 // current step (one row per env).
 __shared__ float s_smp_n[E_WG][KURA_S_MAX + 2];
@@ -205,7 +219,8 @@ __device__ __forceinline__ T* uniform_ptr(T* ptr) {
 // of kura_k1w.inc); wave w owns column tiles w*TPW .. w*TPW+TPW-1 either way.
 template <int TPW, int NWV = NWAVES>
 __device__ __forceinline__ void coupling_gemm(const float* __restrict__ Xs, const float* __restrict__ alpha_sw,
-                                              floatx16 (&acc)[TPW]) {
+                                              floatx16 (&acc)[TPW], unsigned long long* dbg = nullptr) {
+    (void)dbg;  // KURA_DEBUG: bounds flag target
     constexpr int N = TPW * 32 * NWV;
     constexpr int NK8 = N / 8;
     constexpr int TSTRIDE = NK8 * 64;  // floatx4 per column tile
@@ -237,6 +252,8 @@ __device__ __forceinline__ void coupling_gemm(const float* __restrict__ Xs, cons
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
         (void*)(au + (size_t)wave * TPW * TSTRIDE * 4), 0, TPW * TSTRIDE * 16, 0x00020000);
     auto ld = [&](int t, int k) -> floatx4 {
+        KDBG_CHECK(dbg, k >= 0 && k < NK8 && (lane + k * 64) * 16 + t * TSTRIDE * 16 + 16 <=
+                                                                        TPW * TSTRIDE * 16);
         return __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(rs, (lane + k * 64) * 16,
                                                                                  t * TSTRIDE * 16, 0));
     };
@@ -461,8 +478,27 @@ struct Slot {
     int N;
     int ct0;   // first column tile of this wave (wave * TPW), wave-uniform
     int voff;  // lane * 16 bytes (half 0); half 1 at +1024
+#ifdef KURA_DEBUG
+    unsigned long long* stats;  // KURA_DEBUG: bounds flag target
+#endif
     __device__ int soff(int slot, int t) const { return (slot * N + 32 * (ct0 + t)) * 64; }
+    // KURA_DEBUG: the 16 bytes at voff (+1024) + soff lie inside the NSLOT * N * 16 floats of the pair
+    __device__ void check(int slot, int t) const {
+        KDBG_CHECK(stats, slot >= 0 && slot < NSLOT && ct0 + t >= 0 && (ct0 + t) * 32 < N &&
+                              voff + 1024 + soff(slot, t) + 16 <= NSLOT * N * 16 * 4);
+    }
 };
+// the records of workgroup pair `pair`, this wave's tiles from ct0
+__device__ __forceinline__ Slot make_slot(const DevParams& p, int pair, int N, int ct0) {
+    const int lane = threadIdx.x & 63;
+    Slot s{__builtin_amdgcn_make_buffer_rsrc((void*)uniform_ptr(p.R + (size_t)pair * NSLOT * N * 16), 0,
+                                             NSLOT * N * 16 * 4, 0x00020000),
+           N, ct0, lane * 16};
+#ifdef KURA_DEBUG
+    s.stats = uniform_ptr(p.stats);
+#endif
+    return s;
+}
 
 __device__ __forceinline__ void split8(const floatx4& a, const floatx4& b, float (&v)[8]) {
     v[0] = a[0]; v[1] = a[1]; v[2] = a[2]; v[3] = a[3];
@@ -470,6 +506,7 @@ __device__ __forceinline__ void split8(const floatx4& a, const floatx4& b, float
 }
 // lane's two env groups: half 0 -> envs 4h..4h+3, half 1 -> envs 8+4h..8+4h+3
 __device__ __forceinline__ void load8(const Slot& w, int slot, int t, float (&v)[8]) {
+    w.check(slot, t);
     const floatx4 a = __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(w.rs, w.voff, w.soff(slot, t), 0));
     const floatx4 b =
         __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(w.rs, w.voff + 1024, w.soff(slot, t), 0));
@@ -506,6 +543,7 @@ __device__ __forceinline__ void store8(const Slot& w, int slot, int t, const flo
     // (Round 1 used global stores here after an unexplained record loss at
     // N=256 during development; it does not reproduce at the commit that
     // introduced the workaround or at any later one)
+    w.check(slot, t);
     const floatx4 a = {v[0], v[1], v[2], v[3]}, b = {v[4], v[5], v[6], v[7]};
     store_rec_b128(a, w.rs, w.voff, w.soff(slot, t));
     store_rec_b128(b, w.rs, w.voff + 1024, w.soff(slot, t));
@@ -1000,6 +1038,7 @@ __device__ __forceinline__ void save_pass(const DevParams& __restrict__ p, const
                 const float ln = rm_total(e, k) / (float)NG;
                 const double lr = gauss ? 0.0 + rm_total_d(e, k) / (double)NG : (double)ln;
                 const int pos = c.si + r0 + k - c.lfp_from + c.pos0;
+                KDBG_CHECK(p.stats, pos >= 0 && (to_ring ? pos < p.W : pos < KURA_S_MAX + 2) && env_base + e < p.B);
                 if (to_ring) {
                     p.ring[(size_t)(env_base + e) * p.W + pos] = lr;
                 } else {
@@ -1029,6 +1068,7 @@ __device__ __forceinline__ void save_pass(const DevParams& __restrict__ p, const
                 const float ln = ltot[k] / (float)NG;
                 const double lr = gauss ? 0.0 + ltot_d[k] / (double)NG : (double)ln;
                 const int pos = si - c.lfp_from + c.pos0;
+                KDBG_CHECK(p.stats, pos >= 0 && (to_ring ? pos < p.W : pos < KURA_S_MAX + 2) && env_base + tid < p.B);
                 if (to_ring) {
                     if (pt.part == 0) p.ring[(size_t)(env_base + tid) * p.W + pos] = lr;
                 } else {
@@ -1207,9 +1247,7 @@ __device__ void solve_wg(const DevParams& __restrict__ p, float* Xs, int env_bas
     const int col0 = XL ? __builtin_amdgcn_readfirstlane(pt.col0) : 0;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int pair = __builtin_amdgcn_readfirstlane(pt.pair);
-    const Slot ws{__builtin_amdgcn_make_buffer_rsrc((void*)uniform_ptr(p.R + (size_t)pair * NSLOT * N * 16), 0,
-                                                    NSLOT * N * 16 * 4, 0x00020000),
-                  N, wv * TPW, lane * 16};
+    const Slot ws = make_slot(p, pair, N, wv * TPW);
     // records y0 <- state y, omega, pulse (0 while stimulation is OFF, env.py:434)
 #pragma unroll 1
     for (int t = 0; t < TPW; ++t) {
@@ -1249,7 +1287,11 @@ __device__ void solve_wg(const DevParams& __restrict__ p, float* Xs, int env_bas
             xown = xgrp + (size_t)__builtin_amdgcn_readfirstlane(pt.part) * xl_img(TPW);
             coupling_gemm_xl<TPW>(xgrp, p.alpha_sw, Xs, NG, col0, acc);
         } else {
+#ifdef KURA_DEBUG
+            coupling_gemm<TPW>(Xs, p.alpha_sw, acc, uniform_ptr(p.stats));
+#else
             coupling_gemm<TPW>(Xs, p.alpha_sw, acc);
+#endif
         }
         STAMP(2);
         coupling_epilogue<TPW, XL>(p, ws, Xs, xown, acc, s, pulse_on);

@@ -65,8 +65,12 @@ enum {
     KURA_F_MAX_STEPS = 1,   /* diffeqsolve max_steps reached */
     KURA_F_NONFINITE = 2,   /* NaN/Inf state or RHS (non-finite error norm) */
     KURA_F_GRID = 8,        /* save grid outside [2, KURA_S_MAX] samples */
-    KURA_F_BARRIER = 16     /* split-group (N > 1024) barrier timed out: every
-                               exchange after it is unsynchronised */
+    KURA_F_BARRIER = 16,    /* split-group (N > 1024) barrier, or a K1t team
+                               wait, timed out: every exchange after it is
+                               unsynchronised */
+    KURA_F_BOUNDS = 32      /* KURA_DEBUG builds (libkura_debug.so) only: a
+                               record / alpha / ring / sample access outside
+                               its buffer (kura_get_stats()[3]) */
 };
 
 enum { KURA_REC_NAIVE = 0, KURA_REC_GAUSSIAN = 1 };             /* env.py:333-338 */
