@@ -16,6 +16,10 @@ C3) the stimulation field collapses after the first event and HF-DBS stops
 working (10.7e-3 vs the paper's 3.4e-3); reading the config's "[%]" unit
 literally (encapsulation_mode="relative") gives 3.1e-3.  The test asserts
 both, so the divergence stays documented rather than hidden.
+The spread is pinned too: the sd over the five envs of
+every row that meets the mean rule lies within [1/2.5, 2.5] of the paper's
+sd (with five envs the sample sd of a normal population lands inside that
+band with probability > 0.98; measured ratios 1.00-1.52).
 """
 import importlib
 import json
@@ -28,6 +32,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 PAPER = json.load(open(os.path.join(HERE, "golden", "paper_anchors.json")))["anchors"]
 ORACLE = json.load(open(os.path.join(HERE, "golden", "anchor_oracle.json")))["runs"]
 Z_MAX = 1.5
+SD_BAND = 2.5
 
 
 def _run(name, episodes, overrides):
@@ -40,6 +45,10 @@ def _run(name, episodes, overrides):
 def _z(name, arm, values):
     a = PAPER[name][arm]
     return (float(np.mean(values)) - a["mean"]) / a["sd"]
+
+
+def _sd_ratio(name, arm, values):
+    return float(np.std(values, ddof=1)) / PAPER[name][arm]["sd"]
 
 
 def test_paper_table_transcription():
@@ -56,10 +65,12 @@ def test_oracle_protocol_meets_paper(name, overrides):
     r = _run(name, 5, overrides)
     z_off, z_hf = _z(name, "off", r["bbpow_off"]), _z(name, "hf", r["bbpow_hf"])
     assert abs(z_off) <= Z_MAX, (name, z_off)
+    assert 1 / SD_BAND <= _sd_ratio(name, "off", r["bbpow_off"]) <= SD_BAND
     if name == "env2" and not overrides:
         assert z_hf > 5.0, z_hf          # shipped raw encapsulation: HF-DBS collapses (documented divergence)
     else:
         assert abs(z_hf) <= Z_MAX, (name, overrides, z_hf)
+        assert 1 / SD_BAND <= _sd_ratio(name, "hf", r["bbpow_hf"]) <= SD_BAND
 
 
 def test_oracle_protocol_env0_one_episode():
