@@ -159,6 +159,16 @@ __shared__ double s_smp_r[E_WG][KURA_S_MAX + 2];
 #define XL_KC 512                        // oscillators per streamed GEMM chunk
 #define XL_CIMG (XL_KC / 8 * XS_BLOCK)   // floats of one chunk image
 #define XL_SPIN_MAX (1u << 25)
+// alpha ring depth (k-blocks) of the split-group GEMM at TPW = 1 / 2
+#ifndef KURA_XL_DEPTH1
+#define KURA_XL_DEPTH1 8
+#endif
+#ifndef KURA_XL_DEPTH2
+#define KURA_XL_DEPTH2 8
+#endif
+#ifndef KURA_XL_DEPTH4
+#define KURA_XL_DEPTH4 4
+#endif
 __host__ __device__ constexpr int xs_floats(int N) { return (N / 8) * XS_BLOCK; }
 // floats of one part's LDS / global sin/cos image (TPW column tiles per wave)
 __host__ __device__ constexpr int xl_img(int tpw) { return xs_floats(tpw * 256); }
@@ -257,6 +267,34 @@ __device__ __forceinline__ void coupling_gemm(const float* __restrict__ Xs, cons
         return __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(rs, (lane + k * 64) * 16,
                                                                                  t * TSTRIDE * 16, 0));
     };
+#ifdef KURA_G_RING
+    // A/B variant: alpha ring of GD k-blocks, A fragment read one block ahead
+    constexpr int GD = NWV == NWAVES ? KURA_G_RING : 2;
+    floatx4 bq[GD][TPW];
+#pragma unroll
+    for (int d = 0; d < GD; ++d)
+#pragma unroll
+        for (int t = 0; t < TPW; ++t) bq[d][t] = ld(t, d);
+    floatx4 an = xs4[0];
+#pragma unroll 1
+    for (int kb = 0; kb < NK8; kb += GD) {
+#pragma unroll
+        for (int d = 0; d < GD; ++d) {
+            const floatx4 a = an;
+            an = xs4[(kb + d + 1 < NK8 ? kb + d + 1 : NK8 - 1) * (XS_BLOCK / 4)];
+#pragma unroll
+            for (int s = 0; s < 4; ++s)
+#pragma unroll
+                for (int t = 0; t < TPW; ++t)
+                    acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s], bq[d][t][s], acc[t], 0, 0, 0);
+            const int kn = kb + d + GD < NK8 ? kb + d + GD : NK8 - 1;
+#pragma unroll
+            for (int t = 0; t < TPW; ++t) bq[d][t] = ld(t, kn);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+    return;
+#endif
     floatx4 b0[TPW], b1[TPW];
 #pragma unroll
     for (int t = 0; t < TPW; ++t) {
@@ -308,7 +346,7 @@ __device__ __forceinline__ void lds_barrier() {
 // columns (col0 ..) of alpha.
 template <int TPW>
 __device__ __forceinline__ void coupling_gemm_xl(const float* __restrict__ xg, const float* __restrict__ alpha_sw,
-                                                 float* Xs, int NG, int col0, floatx16 (&acc)[TPW]) {
+                                                 float* Xs, int NG, int col0, floatx16 (&acc)[TPW] STAMP_PARAMS) {
     // (xg, NG, col0 arrive through the VGPR-passed Part of the non-inlined
     // solver; they are wave-uniform, readfirstlane makes that provable)
     NG = __builtin_amdgcn_readfirstlane(NG);  // all addressing below must be provably uniform
@@ -338,54 +376,77 @@ __device__ __forceinline__ void coupling_gemm_xl(const float* __restrict__ xg, c
     floatx4* xs4w = (floatx4*)Xs;
     for (int k = threadIdx.x; k < C4; k += NTHREADS) xs4w[k] = xg4[k];
     lds_barrier();
-    floatx4 b0[TPW], b1[TPW];
+    STAMP(18);  // split groups: chunk 0 staged (slot 18 is free outside KURA_STAMPS_SI)
+    // alpha ring of XD k-blocks per tile: the load of k-block kb + XD is
+    // issued right after the MFMAs of kb, so it has XD - 1 k-blocks of this
+    // wave's and its SIMD partner's MFMAs to arrive.  With TPW = 4 a k-block is
+    // 16 MFMAs per wave and XD = 2 covers the L2 latency; at TPW = 1 (parts of
+    // 256) a k-block is only 4 MFMAs, and a ring of 2 left the MFMAs waiting on
+    // alpha (DESIGN.md section 5, K1').  The ring costs XD * TPW * 4 VGPRs.
+    constexpr int XD = TPW >= 4 ? KURA_XL_DEPTH4 : (TPW == 2 ? KURA_XL_DEPTH2 : KURA_XL_DEPTH1);
+    constexpr int KPC = XL_KC / 8;                 // k-blocks per chunk
+    constexpr int PRE = (CPT + XD - 1) / XD * XD;  // unrolled head: one staging load per k-block
+    static_assert(KPC % XD == 0 && PRE <= KPC, "alpha ring must tile the chunk");
+    floatx4 bq[XD][TPW];
 #pragma unroll
-    for (int t = 0; t < TPW; ++t) {
-        b0[t] = ld(t, 0);
-        b1[t] = ld(t, 1);
-    }
-    // one k-block pair of this chunk (k-blocks kb, kb+1 local; kg0 + .. global)
-    auto kpair = [&](const floatx4* xs4, int kg0, int kb) __attribute__((always_inline)) {
-        floatx4 a = xs4[kb * (XS_BLOCK / 4)];
+    for (int d = 0; d < XD; ++d)
+#pragma unroll
+        for (int t = 0; t < TPW; ++t) bq[d][t] = ld(t, d);
+    // k-block kb (local) of the chunk whose LDS image is xs4, ring slot d = kb % XD;
+    // the A fragment of the next k-block is read from LDS one block ahead
+    floatx4 an, an0;
+    (void)an0;
+    auto kblock = [&](const floatx4* xs4, int kg0, int kb, int d) __attribute__((always_inline)) {
+#ifdef KURA_XL_A2
+        const floatx4 a = an0;
+        an0 = an;
+        an = xs4[(kb + 2 < KPC ? kb + 2 : KPC - 1) * (XS_BLOCK / 4)];
+#else
+        const floatx4 a = an;
+        an = xs4[(kb + 1 < KPC ? kb + 1 : KPC - 1) * (XS_BLOCK / 4)];
+#endif
 #pragma unroll
         for (int s = 0; s < 4; ++s)
 #pragma unroll
             for (int t = 0; t < TPW; ++t)
-                acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s], b0[t][s], acc[t], 0, 0, 0);
-        const int k2 = kg0 + kb + 2 < NK8 ? kg0 + kb + 2 : NK8 - 1;
+                acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s], bq[d][t][s], acc[t], 0, 0, 0);
+        const int kn = kg0 + kb + XD < NK8 ? kg0 + kb + XD : NK8 - 1;
 #pragma unroll
-        for (int t = 0; t < TPW; ++t) b0[t] = ld(t, k2);
-        __builtin_amdgcn_sched_barrier(0);
-        a = xs4[(kb + 1) * (XS_BLOCK / 4)];
-#pragma unroll
-        for (int s = 0; s < 4; ++s)
-#pragma unroll
-            for (int t = 0; t < TPW; ++t)
-                acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s], b1[t][s], acc[t], 0, 0, 0);
-        const int k3 = kg0 + kb + 3 < NK8 ? kg0 + kb + 3 : NK8 - 1;
-#pragma unroll
-        for (int t = 0; t < TPW; ++t) b1[t] = ld(t, k3);
-        __builtin_amdgcn_sched_barrier(0);
+        for (int t = 0; t < TPW; ++t) bq[d][t] = ld(t, kn);
     };
 #pragma unroll 1
     for (int c = 0; c < nchunk; ++c) {
         const floatx4* xs4 = reinterpret_cast<const floatx4*>(Xs + (c & 1) * XL_CIMG + (lane >> 5) * XS_HALF +
                                                               (lane & 31) * 4);
-        const int kg0 = c * (XL_KC / 8);
+        const int kg0 = c * KPC;
         const bool more = c + 1 < nchunk;
-        // the next chunk is staged in registers one float4 per k-block pair,
-        // each load issued right after that pair's alpha loads, so the
-        // in-order vmcnt waits of later pairs cover it without a stall
+#ifdef KURA_XL_A2
+        an0 = xs4[0];
+        an = xs4[XS_BLOCK / 4];
+#else
+        an = xs4[0];
+#endif
+        // the next chunk is staged in registers one float4 per k-block, each
+        // load issued right after that block's alpha loads, so the in-order
+        // vmcnt waits of later blocks cover it without a stall
         floatx4 nx[CPT];
 #pragma unroll
-        for (int u = 0; u < CPT; ++u) {
-            kpair(xs4, kg0, 2 * u);
-            const int k = threadIdx.x + u * NTHREADS;
-            if (more && k < C4) nx[u] = xg4[(size_t)(c + 1) * C4 + k];
+        for (int kb = 0; kb < PRE; ++kb) {
+            kblock(xs4, kg0, kb, kb % XD);
+            const int k = threadIdx.x + kb * NTHREADS;
+            if (kb < CPT && more && k < C4) nx[kb] = xg4[(size_t)(c + 1) * C4 + k];
             __builtin_amdgcn_sched_barrier(0);
         }
 #pragma unroll 1
-        for (int kb = 2 * CPT; kb < XL_KC / 8; kb += 2) kpair(xs4, kg0, kb);
+        for (int kb = PRE; kb < KPC; kb += XD) {
+#pragma unroll
+            for (int d = 0; d < XD; ++d) {
+                kblock(xs4, kg0, kb + d, d);
+#ifndef KURA_XL_NOSB
+                __builtin_amdgcn_sched_barrier(0);
+#endif
+            }
+        }
         if (more) {  // the other buffer was last read in chunk c-1, before the previous barrier
             floatx4* dst = (floatx4*)(Xs + ((c + 1) & 1) * XL_CIMG);
 #pragma unroll
@@ -394,7 +455,9 @@ __device__ __forceinline__ void coupling_gemm_xl(const float* __restrict__ xg, c
                 if (k < C4) dst[k] = nx[u];
             }
         }
+        STAMP(2);
         lds_barrier();
+        STAMP(17);  // split groups: chunk barrier wait (slot 17 is free outside KURA_STAMPS_SI)
     }
 }
 
@@ -1285,7 +1348,8 @@ __device__ void solve_wg(const DevParams& __restrict__ p, float* Xs, int env_bas
         if constexpr (XL) {
             const float* xgrp = uniform_ptr(group_publish_x<TPW>(p, pt, Xs));   // all parts' images of this stage
             xown = xgrp + (size_t)__builtin_amdgcn_readfirstlane(pt.part) * xl_img(TPW);
-            coupling_gemm_xl<TPW>(xgrp, p.alpha_sw, Xs, NG, col0, acc);
+            STAMP(16);  // split groups: image publish + group barrier (slot 16 is free outside KURA_STAMPS_SI)
+            coupling_gemm_xl<TPW>(xgrp, p.alpha_sw, Xs, NG, col0, acc STAMP_ARGS);
         } else {
 #ifdef KURA_DEBUG
             coupling_gemm<TPW>(Xs, p.alpha_sw, acc, uniform_ptr(p.stats));
