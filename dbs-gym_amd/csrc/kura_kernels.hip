@@ -267,34 +267,6 @@ __device__ __forceinline__ void coupling_gemm(const float* __restrict__ Xs, cons
         return __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(rs, (lane + k * 64) * 16,
                                                                                  t * TSTRIDE * 16, 0));
     };
-#ifdef KURA_G_RING
-    // A/B variant: alpha ring of GD k-blocks, A fragment read one block ahead
-    constexpr int GD = NWV == NWAVES ? KURA_G_RING : 2;
-    floatx4 bq[GD][TPW];
-#pragma unroll
-    for (int d = 0; d < GD; ++d)
-#pragma unroll
-        for (int t = 0; t < TPW; ++t) bq[d][t] = ld(t, d);
-    floatx4 an = xs4[0];
-#pragma unroll 1
-    for (int kb = 0; kb < NK8; kb += GD) {
-#pragma unroll
-        for (int d = 0; d < GD; ++d) {
-            const floatx4 a = an;
-            an = xs4[(kb + d + 1 < NK8 ? kb + d + 1 : NK8 - 1) * (XS_BLOCK / 4)];
-#pragma unroll
-            for (int s = 0; s < 4; ++s)
-#pragma unroll
-                for (int t = 0; t < TPW; ++t)
-                    acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s], bq[d][t][s], acc[t], 0, 0, 0);
-            const int kn = kb + d + GD < NK8 ? kb + d + GD : NK8 - 1;
-#pragma unroll
-            for (int t = 0; t < TPW; ++t) bq[d][t] = ld(t, kn);
-            __builtin_amdgcn_sched_barrier(0);
-        }
-    }
-    return;
-#endif
     floatx4 b0[TPW], b1[TPW];
 #pragma unroll
     for (int t = 0; t < TPW; ++t) {
@@ -394,17 +366,10 @@ __device__ __forceinline__ void coupling_gemm_xl(const float* __restrict__ xg, c
         for (int t = 0; t < TPW; ++t) bq[d][t] = ld(t, d);
     // k-block kb (local) of the chunk whose LDS image is xs4, ring slot d = kb % XD;
     // the A fragment of the next k-block is read from LDS one block ahead
-    floatx4 an, an0;
-    (void)an0;
+    floatx4 an;
     auto kblock = [&](const floatx4* xs4, int kg0, int kb, int d) __attribute__((always_inline)) {
-#ifdef KURA_XL_A2
-        const floatx4 a = an0;
-        an0 = an;
-        an = xs4[(kb + 2 < KPC ? kb + 2 : KPC - 1) * (XS_BLOCK / 4)];
-#else
         const floatx4 a = an;
         an = xs4[(kb + 1 < KPC ? kb + 1 : KPC - 1) * (XS_BLOCK / 4)];
-#endif
 #pragma unroll
         for (int s = 0; s < 4; ++s)
 #pragma unroll
@@ -420,12 +385,7 @@ __device__ __forceinline__ void coupling_gemm_xl(const float* __restrict__ xg, c
                                                               (lane & 31) * 4);
         const int kg0 = c * KPC;
         const bool more = c + 1 < nchunk;
-#ifdef KURA_XL_A2
-        an0 = xs4[0];
-        an = xs4[XS_BLOCK / 4];
-#else
         an = xs4[0];
-#endif
         // the next chunk is staged in registers one float4 per k-block, each
         // load issued right after that block's alpha loads, so the in-order
         // vmcnt waits of later blocks cover it without a stall
@@ -442,9 +402,7 @@ __device__ __forceinline__ void coupling_gemm_xl(const float* __restrict__ xg, c
 #pragma unroll
             for (int d = 0; d < XD; ++d) {
                 kblock(xs4, kg0, kb + d, d);
-#ifndef KURA_XL_NOSB
                 __builtin_amdgcn_sched_barrier(0);
-#endif
             }
         }
         if (more) {  // the other buffer was last read in chunk c-1, before the previous barrier
