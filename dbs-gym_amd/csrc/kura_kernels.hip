@@ -980,65 +980,92 @@ __device__ __forceinline__ void save_pass(const DevParams& __restrict__ p, const
     // evaluated without branching (rows that are not saved or feed no LFP
     // sample are computed and discarded by a select: the partial sums see
     // exactly the additions of the branchy form, in the same order)
+    // Tiles are visited one 16-byte record half at a time (envs q = 4h..4h+3),
+    // all TPW tiles of half 0, then of half 1, with the five records of the
+    // next (tile, half) in flight while the current one is evaluated.  Every
+    // (round, env) partial still adds its tiles in t order, so the sums are
+    // those of a tile-by-tile pass (bit-exact); a prefetched half costs the
+    // registers one whole tile used to.
+    if (eval_rows) {
+        float rc[5][4];  // CA, CB, CC, F0, Y0 of the current (tile, half)
+        auto load_half = [&](int t, int hh, float (&r)[5][4]) __attribute__((always_inline)) {
+            const int sl[5] = {SL_CA, SL_CB, SL_CC, SL_F0, SL_Y0};
+#pragma unroll
+            for (int j = 0; j < 5; ++j) {
+                ws.check(sl[j], t);
+                const floatx4 v = __builtin_bit_cast(
+                    floatx4, __builtin_amdgcn_raw_buffer_load_b128(ws.rs, ws.voff, ws.soff(sl[j], t) + hh * 1024, 0));
+                r[j][0] = v[0]; r[j][1] = v[1]; r[j][2] = v[2]; r[j][3] = v[3];
+            }
+        };
+        load_half(0, 0, rc);
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
 #pragma unroll 1
-    for (int t = 0; t < (eval_rows ? TPW : 0); ++t) {
-        const int i = 32 * (wave * TPW + t) + (lane & 31);
-        float ca[8], cb[8], cc[8], f0[8], y0[8];
-        double G[8];
-        load8(ws, SL_CA, t, ca);
-        load8(ws, SL_CB, t, cb);
-        load8(ws, SL_CC, t, cc);
-        load8(ws, SL_F0, t, f0);
-        load8(ws, SL_Y0, t, y0);
-        if (gauss) {
+            for (int t = 0; t < TPW; ++t) {
+                const int i = 32 * (wave * TPW + t) + (lane & 31);
+                const bool last = t + 1 == TPW;
+                float rn[5][4];
+                if (!(hh == 1 && last)) load_half(last ? 0 : t + 1, last ? 1 : hh, rn);
+                double G[4];
+                if (gauss) {
 #pragma unroll
-            for (int q = 0; q < 8; ++q) {
-                int env = env_base + mfma_env(q, lane);
-                env = env < Bn ? env : Bn - 1;
-                G[q] = p.g_rec[(size_t)env * NG + col0 + i];
-            }
-        }
+                    for (int qq = 0; qq < 4; ++qq) {
+                        int env = env_base + mfma_env(4 * hh + qq, lane);
+                        env = env < Bn ? env : Bn - 1;
+                        G[qq] = p.g_rec[(size_t)env * NG + col0 + i];
+                    }
+                }
 #ifdef KURA_STAMPS
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // attribute the record-load wait (diagnostic build)
-        STAMP(12);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // attribute the record-load wait (diagnostic build)
+                STAMP(12);
 #endif
-        float k0[8];
+                float k0[4];
 #pragma unroll
-        for (int q = 0; q < 8; ++q) k0[q] = h[q] * f0[q];
+                for (int qq = 0; qq < 4; ++qq) k0[qq] = h[4 * hh + qq] * rc[3][qq];
 #pragma unroll
-        for (int k = 0; k < RCX; ++k) {
-            if (k >= nk) break;  // wave-uniform: past every env's last save of this step
-            float v[8];
+                for (int k = 0; k < RCX; ++k) {
+                    if (k >= nk) break;  // wave-uniform: past every env's last save of this step
+                    float v[4];
 #pragma unroll
-            for (int q = 0; q < 8; ++q) {
-                const int f = fl[q] >> (3 * k);
-                const float x = th[k][q];
-                float w = ca[q] * x + cb[q];
-                w = w * x + cc[q];
-                w = w * x + k0[q];
-                w = w * x + y0[q];
-                v[q] = w;
-                const float cr = kdm_cosf(w);
-                pn[k][q] = (f & 2) ? pn[k][q] + cr : pn[k][q];
-                if (gauss) pg[k][q] = (f & 2) ? pg[k][q] + (double)cr * G[q] : pg[k][q];
-            }
-            if ((fin >> k) & 1) {  // the solve's last row: the new state
+                    for (int qq = 0; qq < 4; ++qq) {
+                        const int q = 4 * hh + qq;
+                        const int f = fl[q] >> (3 * k);
+                        const float x = th[k][q];
+                        float w = rc[0][qq] * x + rc[1][qq];
+                        w = w * x + rc[2][qq];
+                        w = w * x + k0[qq];
+                        w = w * x + rc[4][qq];
+                        v[qq] = w;
+                        const float cr = kdm_cosf(w);
+                        pn[k][q] = (f & 2) ? pn[k][q] + cr : pn[k][q];
+                        if (gauss) pg[k][q] = (f & 2) ? pg[k][q] + (double)cr * G[qq] : pg[k][q];
+                    }
+                    if ((fin >> k) & 1) {  // the solve's last row: the new state
 #pragma unroll
-                for (int q = 0; q < 8; ++q) {
-                    const int env = env_base + mfma_env(q, lane);
-                    if (((fl[q] >> (3 * k)) & 4) && env < Bn) yout[(size_t)env * NG + col0 + i] = v[q];
+                        for (int qq = 0; qq < 4; ++qq) {
+                            const int q = 4 * hh + qq;
+                            const int env = env_base + mfma_env(q, lane);
+                            if (((fl[q] >> (3 * k)) & 4) && env < Bn) yout[(size_t)env * NG + col0 + i] = v[qq];
+                        }
+                    }
+                    if (capture) {
+#pragma unroll
+                        for (int qq = 0; qq < 4; ++qq) {
+                            const int q = 4 * hh + qq;
+                            const int env = env_base + mfma_env(q, lane);
+                            if (((fl[q] >> (3 * k)) & 1) && env < Bn)
+                                rows[((size_t)env * (KURA_S_MAX + 1) + rbase[q] + k) * NG + col0 + i] = v[qq];
+                        }
+                    }
                 }
-            }
-            if (capture) {
 #pragma unroll
-                for (int q = 0; q < 8; ++q) {
-                    const int env = env_base + mfma_env(q, lane);
-                    if (((fl[q] >> (3 * k)) & 1) && env < Bn)
-                        rows[((size_t)env * (KURA_S_MAX + 1) + rbase[q] + k) * NG + col0 + i] = v[q];
-                }
+                for (int j = 0; j < 5; ++j)
+#pragma unroll
+                    for (int qq = 0; qq < 4; ++qq) rc[j][qq] = rn[j][qq];
+                STAMP(13);
             }
         }
-        STAMP(13);
     }
 #pragma unroll
     for (int k = 0; k < RCX; ++k) {

@@ -11,7 +11,8 @@ for lib in "$@"; do
   timeout -k 10 150 python3 -u tools/parity_probe.py env1 1024 19 3 rand $R/$C/$lib > $O/probe_${lib%.so}.txt 2>&1; rc=$?
   [ $rc -eq 0 ] || { echo "$lib probe rc=$rc"; cat $O/probe_${lib%.so}.txt | tail -5; exit $rc; }
   if ! grep -q "all equal" $O/probe_${lib%.so}.txt; then echo "$lib MISMATCH"; continue; fi
-  cp $C/$lib $C/libkura.so
+  # (libkura.so itself: the production build saved above, not whatever was copied over it last)
+  if [ $lib = libkura.so ]; then cp $C/libkura_orig.so $C/libkura.so; else cp $C/$lib $C/libkura.so; fi
   timeout -k 10 300 python bench.py --steps 20 --warmup 5 --cpu-seconds 0 > $O/bench_${lib%.so}.json 2> $O/bench_${lib%.so}.err; rc=$?
   [ $rc -eq 0 ] || { echo "$lib bench rc=$rc"; exit $rc; }
   python3 -c "import json;d=json.loads(open('$O/bench_${lib%.so}.json').readline());print('$lib',d['value'],d['ms_per_step'],d['roofline']['avg_kernel_ms'],d['extra']['reset_ms'])"
