@@ -980,13 +980,16 @@ __device__ __forceinline__ void save_pass(const DevParams& __restrict__ p, const
     // evaluated without branching (rows that are not saved or feed no LFP
     // sample are computed and discarded by a select: the partial sums see
     // exactly the additions of the branchy form, in the same order)
-    // Tiles are visited one 16-byte record half at a time (envs q = 4h..4h+3),
+    // Split groups: tiles are visited one 16-byte record half at a time (envs q = 4h..4h+3),
     // all TPW tiles of half 0, then of half 1, with the five records of the
     // next (tile, half) in flight while the current one is evaluated.  Every
     // (round, env) partial still adds its tiles in t order, so the sums are
     // those of a tile-by-tile pass (bit-exact); a prefetched half costs the
     // registers one whole tile used to.
-    if (eval_rows) {
+    // (K1 / K2 keep the tile-by-tile pass: same-box A/B, the half-tile form
+    // cost the N=1024 step 0.5 % and gained its reset 0.4 %,
+    // profiles/r03_savepass_ab.txt; the split strong form gained 1.5 %)
+    if (XL && eval_rows) {
         float rc[5][4];  // CA, CB, CC, F0, Y0 of the current (tile, half)
         auto load_half = [&](int t, int hh, float (&r)[5][4]) __attribute__((always_inline)) {
             const int sl[5] = {SL_CA, SL_CB, SL_CC, SL_F0, SL_Y0};
@@ -1066,6 +1069,66 @@ __device__ __forceinline__ void save_pass(const DevParams& __restrict__ p, const
                 STAMP(13);
             }
         }
+    }
+#pragma unroll 1
+    for (int t = 0; t < (!XL && eval_rows ? TPW : 0); ++t) {
+        const int i = 32 * (wave * TPW + t) + (lane & 31);
+        float ca[8], cb[8], cc[8], f0[8], y0[8];
+        double G[8];
+        load8(ws, SL_CA, t, ca);
+        load8(ws, SL_CB, t, cb);
+        load8(ws, SL_CC, t, cc);
+        load8(ws, SL_F0, t, f0);
+        load8(ws, SL_Y0, t, y0);
+        if (gauss) {
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                int env = env_base + mfma_env(q, lane);
+                env = env < Bn ? env : Bn - 1;
+                G[q] = p.g_rec[(size_t)env * NG + col0 + i];
+            }
+        }
+#ifdef KURA_STAMPS
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // attribute the record-load wait (diagnostic build)
+        STAMP(12);
+#endif
+        float k0[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) k0[q] = h[q] * f0[q];
+#pragma unroll
+        for (int k = 0; k < RCX; ++k) {
+            if (k >= nk) break;  // wave-uniform: past every env's last save of this step
+            float v[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                const int f = fl[q] >> (3 * k);
+                const float x = th[k][q];
+                float w = ca[q] * x + cb[q];
+                w = w * x + cc[q];
+                w = w * x + k0[q];
+                w = w * x + y0[q];
+                v[q] = w;
+                const float cr = kdm_cosf(w);
+                pn[k][q] = (f & 2) ? pn[k][q] + cr : pn[k][q];
+                if (gauss) pg[k][q] = (f & 2) ? pg[k][q] + (double)cr * G[q] : pg[k][q];
+            }
+            if ((fin >> k) & 1) {  // the solve's last row: the new state
+#pragma unroll
+                for (int q = 0; q < 8; ++q) {
+                    const int env = env_base + mfma_env(q, lane);
+                    if (((fl[q] >> (3 * k)) & 4) && env < Bn) yout[(size_t)env * NG + col0 + i] = v[q];
+                }
+            }
+            if (capture) {
+#pragma unroll
+                for (int q = 0; q < 8; ++q) {
+                    const int env = env_base + mfma_env(q, lane);
+                    if (((fl[q] >> (3 * k)) & 1) && env < Bn)
+                        rows[((size_t)env * (KURA_S_MAX + 1) + rbase[q] + k) * NG + col0 + i] = v[q];
+                }
+            }
+        }
+        STAMP(13);
     }
 #pragma unroll
     for (int k = 0; k < RCX; ++k) {
