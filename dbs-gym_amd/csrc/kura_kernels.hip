@@ -446,7 +446,7 @@ __shared__ double s_redd[RC][NWAVES][E_WG];      // per-wave partial sums (f64, 
 __shared__ float s_theta[E_WG][RC_N];            // dense-output abscissae of the rounds of a pass
 __shared__ int s_rflag[E_WG][RC_N];              // bit0: save row, bit1: LFP row, bit2: final row
 __shared__ double s_u[E_WG][4];                  // rescaled amplitudes (env.py:389-393)
-__shared__ int s_maxsave, s_any;
+__shared__ int s_maxsave, s_any, s_fsal;
 __shared__ int s_nI[E_WG], s_nII[E_WG];          // ON / OFF grid lengths of the step (step_pair)
 
 __device__ __forceinline__ double grid_at_c(const CtlE& c, int i) {
@@ -499,10 +499,18 @@ struct Slot {
     int N;
     int ct0;   // first column tile of this wave (wave * TPW), wave-uniform
     int voff;  // lane * 16 bytes (half 0); half 1 at +1024
+    // FSAL by renaming (post_step): when every active env of the workgroup
+    // accepts its step, y0 <- y1 and f0 <- f6 swap the two slot pairs instead
+    // of copying records; par = 1 while they are swapped (wave-uniform)
+    int par;
 #ifdef KURA_DEBUG
     unsigned long long* stats;  // KURA_DEBUG: bounds flag target
 #endif
-    __device__ int soff(int slot, int t) const { return (slot * N + 32 * (ct0 + t)) * 64; }
+    __device__ int phys(int slot) const {
+        const int sw = slot == SL_Y0 ? SL_Y1 : slot == SL_Y1 ? SL_Y0 : slot == SL_F0 ? SL_F0 + 6 : slot == SL_F0 + 6 ? SL_F0 : slot;
+        return par ? sw : slot;
+    }
+    __device__ int soff(int slot, int t) const { return (phys(slot) * N + 32 * (ct0 + t)) * 64; }
     // KURA_DEBUG: the 16 bytes at voff (+1024) + soff lie inside the NSLOT * N * 16 floats of the pair
     __device__ void check(int slot, int t) const {
         KDBG_CHECK(stats, slot >= 0 && slot < NSLOT && ct0 + t >= 0 && (ct0 + t) * 32 < N &&
@@ -514,7 +522,7 @@ __device__ __forceinline__ Slot make_slot(const DevParams& p, int pair, int N, i
     const int lane = threadIdx.x & 63;
     Slot s{__builtin_amdgcn_make_buffer_rsrc((void*)uniform_ptr(p.R + (size_t)pair * NSLOT * N * 16), 0,
                                              NSLOT * N * 16 * 4, 0x00020000),
-           N, ct0, lane * 16};
+           N, ct0, lane * 16, 0};
 #ifdef KURA_DEBUG
     s.stats = uniform_ptr(p.stats);
 #endif
@@ -1194,7 +1202,7 @@ __device__ __forceinline__ void save_pass(const DevParams& __restrict__ p, const
 }
 
 template <int TPW, bool XL>
-__device__ __forceinline__ void post_step(const DevParams& __restrict__ p, const Slot& ws, int env_base, bool to_ring, Part& pt
+__device__ __forceinline__ void post_step(const DevParams& __restrict__ p, Slot& ws, int env_base, bool to_ring, Part& pt
                                           STAMP_PARAMS) {
     const int lane = threadIdx.x & 63, tid = threadIdx.x;
     const int NG = XL ? __builtin_amdgcn_readfirstlane(pt.ng) : TPW * 256;   // oscillators per env
@@ -1284,9 +1292,20 @@ __device__ __forceinline__ void post_step(const DevParams& __restrict__ p, const
     }
     lds_barrier();
     if (tid == 0) {
-        int m = 0;
-        for (int e = 0; e < E_WG; ++e) m = s_ctl[e].nsave > m ? s_ctl[e].nsave : m;
+        // most save rounds of any env; FSAL mode: 0 no active env accepts
+        // (nothing to move), 2 every active env accepts (rename the slot
+        // pairs), 1 mixed (select-copy)
+        int m = 0, allk = 1, anyk = 0;
+        for (int e = 0; e < E_WG; ++e) {
+            const CtlE& c = s_ctl[e];
+            m = c.nsave > m ? c.nsave : m;
+            if (c.active) {
+                allk &= c.keep;
+                anyk |= c.keep;
+            }
+        }
         s_maxsave = m;
+        s_fsal = anyk ? (allk ? 2 : 1) : 0;
     }
     lds_barrier();
     STAMP(7);
@@ -1304,12 +1323,16 @@ __device__ __forceinline__ void post_step(const DevParams& __restrict__ p, const
             save_pass<TPW, XL, RC_N>(p, ws, env_base, to_ring, pt, h, r0, nrounds, false STAMP_ARGS);
     }
     STAMP(8);
-    // (4) accepted envs: y0 <- y1, f0 <- f6 (FSAL)
+    // (4) accepted envs: y0 <- y1, f0 <- f6 (FSAL).  Envs that are not
+    // active any more never read their records again (their final state is
+    // out), so when every active env accepts the slot pairs are renamed.
     int kp[8];
 #pragma unroll
     for (int q = 0; q < 8; ++q) kp[q] = s_ctl[mfma_env(q, lane)].keep;
+    const int fmode = __builtin_amdgcn_readfirstlane(s_fsal);
+    if (fmode == 2) ws.par ^= 1;
 #pragma unroll 1
-    for (int t = 0; t < TPW; ++t) {
+    for (int t = 0; t < (fmode == 1 ? TPW : 0); ++t) {
         float y0[8], y1[8], f0[8], f6[8];
         load8(ws, SL_Y0, t, y0);
         load8(ws, SL_Y1, t, y1);
@@ -1358,7 +1381,7 @@ __device__ void solve_wg(const DevParams& __restrict__ p, float* Xs, int env_bas
     const int col0 = XL ? __builtin_amdgcn_readfirstlane(pt.col0) : 0;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int pair = __builtin_amdgcn_readfirstlane(pt.pair);
-    const Slot ws = make_slot(p, pair, N, wv * TPW);
+    Slot ws = make_slot(p, pair, N, wv * TPW);
     // records y0 <- state y, omega, pulse (0 while stimulation is OFF, env.py:434)
 #pragma unroll 1
     for (int t = 0; t < TPW; ++t) {
