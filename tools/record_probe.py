@@ -6,7 +6,10 @@ after that many Dopri steps: flag MAX_STEPS) through K1 (KURA_KERNEL=k1) and
 K1w, copies each one's solver workspace (kura_debug_read_workspace) and
 prints, for the first max_steps where they differ, every record slot that
 differs with its (env, column) positions.  Slots Y0/F0 are skipped (K1
-applies FSAL inside post_step, K1w only before the next attempt).
+applies FSAL inside post_step, K1w only before the next attempt).  Since the
+FSAL renaming (Slot::par) K1's physical slots Y0<->Y1 and F0<->F6 are swapped
+after an odd number of all-accepted steps: compare at max_steps = 1 or read
+the swapped pairs accordingly.
 Usage: [LIB=libkura_x.so] record_probe.py ENV N B [KMAX]"""
 import ctypes
 import importlib
