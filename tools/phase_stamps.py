@@ -43,7 +43,7 @@ def main():
         config = os.environ.get("CFG", "env0")
         osc = int(os.environ.get("OSC", "1024"))
         envs = int(os.environ.get("ENVS", "4096"))
-        reward = "bbpow_action"
+        reward = os.environ.get("REWARD", "bbpow_action")
         seed = 7
         random_k = False
     cfg, alpha, omega, gs, gr, th0, ct, st, gain = bench.build_shard(A, 0)
