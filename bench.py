@@ -8,10 +8,15 @@ the beta-band reward.  Workload: BASELINE.json configs[1] -- env0, N=1024
 oscillators x 4096 envs per GPU, synthetic (random-seeded natural
 frequencies / initial phases, reference grid coupling), actions U(-1, 1).
 
-Multi-GPU: one process per GPU (torchrun), each owning its own shard of
-4096 envs (global env id = rank*B + b seeds the env), no data-path
-collective; the only collectives are the barrier and the max-over-ranks of
-the timed region (weak scaling).
+Multi-GPU: one process per GPU, each owning its own shard of 4096 envs
+(global env id = rank*B + b seeds the env), no data-path collective; the only
+collectives are the barrier and the max-over-ranks of the timed region (weak
+scaling).  Either torchrun starts the ranks (WORLD_SIZE set; it must equal
+--gpus), or `python bench.py --gpus N` does: the parent process never touches
+the GPU, spawns N rank processes with RANK / LOCAL_RANK / WORLD_SIZE /
+MASTER_* set (127.0.0.1), relays rank 0's JSON line and exits non-zero if any
+rank fails.  The line reports the world size the process group saw and every
+rank's own rate.
 """
 from __future__ import annotations
 
@@ -31,7 +36,7 @@ PEAK_FP32_TFLOPS = 157.3   # MI355X dense FP32 (vector == matrix), MI355X_MICROA
 PEAK_HBM_GBS = 8000.0
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -58,7 +63,11 @@ def parse():
     # barrier / max-over-ranks (RCCL cannot put two ranks on one device)
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"])
     ap.add_argument("--share-device", action="store_true", help="every rank uses cuda:0 (rehearsal only)")
-    return ap.parse_args()
+    ap.add_argument("--launcher-selftest", action="store_true",
+                    help="(CPU test of the --gpus N launcher) ranks only join the process group and report")
+    ap.add_argument("--rank-timeout", type=float, default=1800.0,
+                    help="launcher: seconds before the spawned ranks are killed")
+    return ap.parse_args(argv)
 
 
 def build_shard(args, rank):
@@ -287,16 +296,104 @@ def episode_bench(args, rank, world, local_rank):
             "setup_s": setup_s}
 
 
-def main():
-    args = parse()
-    import torch
-    import torch.distributed as dist
+def _free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
 
+
+def launch(args, argv) -> int:
+    """`bench.py --gpus N` without torchrun: start N rank processes of this
+    script (RANK = LOCAL_RANK = r, WORLD_SIZE = N, MASTER_ADDR 127.0.0.1 and a
+    free port), relay rank 0's JSON line, return the first failing rank's exit
+    status (killing the other ranks) or 0.  This process never initialises the
+    GPU: it only counts devices (torch.cuda.device_count() does not initialise
+    HIP on this image) and execs nothing."""
+    import subprocess
+    n = args.gpus
+    if not args.launcher_selftest:
+        import torch
+        ndev = torch.cuda.device_count()
+        need = 1 if args.share_device else n
+        if ndev < need:
+            print(f"[bench] --gpus {n} needs {need} visible GPU(s), {ndev} visible", file=sys.stderr)
+            return 2
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=env,
+                                      stdout=subprocess.PIPE if r == 0 else sys.stderr.fileno()))
+    deadline = time.time() + args.rank_timeout
+    rc = 0
+    while True:
+        codes = [p.poll() for p in procs]
+        bad = [(r, c) for r, c in enumerate(codes) if c not in (None, 0)]
+        late = time.time() > deadline
+        if bad or late:
+            rc = 124 if not bad else (bad[0][1] if bad[0][1] > 0 else 128 - bad[0][1])
+            print(f"[bench] {'rank %d exited with %s' % bad[0] if bad else 'rank timeout'}; stopping the other ranks",
+                  file=sys.stderr)
+            for p in procs:
+                if p.poll() is None:
+                    p.kill()
+            break
+        if all(c == 0 for c in codes):
+            break
+        time.sleep(0.2)
+    for p in procs:
+        p.wait()
+    out = procs[0].stdout.read().decode()
+    procs[0].stdout.close()
+    if out:
+        sys.stdout.write(out)
+        sys.stdout.flush()
+    return rc
+
+
+def launcher_selftest(world, rank, local_rank):
+    """--launcher-selftest: the rank joins the (gloo) process group and rank 0
+    reports who joined -- the CPU test of the launcher (no GPU)."""
+    import torch.distributed as dist
+    if world > 1:
+        dist.init_process_group("gloo")
+    if os.environ.get("KURA_BENCH_FAIL_RANK") == str(rank):   # test hook: a failing rank
+        sys.exit(3)
+    me = {"rank": rank, "local_rank": local_rank, "pid": os.getpid()}
+    ranks = [None] * world
+    if world > 1:
+        dist.all_gather_object(ranks, me)
+    else:
+        ranks = [me]
+    if rank == 0:
+        print(json.dumps({"launcher_selftest": True, "n_gpus": world,
+                          "dist_world_size": dist.get_world_size() if world > 1 else 1, "ranks": ranks}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else list(argv)
+    args = parse(argv)
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch(args, argv))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = 0 if args.share_device else int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and rank == 0:
-        print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+    if world != args.gpus:
+        print(f"[bench] --gpus {args.gpus} but WORLD_SIZE={world}: refusing to report a different GPU count",
+              file=sys.stderr)
+        sys.exit(2)
+    if args.launcher_selftest:
+        launcher_selftest(world, rank, local_rank)
+        return
+    import torch
+    import torch.distributed as dist
+    if not args.share_device and local_rank >= torch.cuda.device_count():
+        print(f"[bench] LOCAL_RANK={local_rank} but {torch.cuda.device_count()} visible GPU(s)", file=sys.stderr)
+        sys.exit(2)
     # CPU baseline first: the reference-op leg forks worker processes, which
     # must happen before this process initialises the GPU
     cpu = cpu_baseline(args) if (world == 1 and args.cpu_seconds > 0) else None
@@ -364,10 +461,15 @@ def main():
     useful_rhs = 2 * B + 6 * steps_attempted
     lockstep_eff = useful_rhs / (16.0 * wg_sweeps) if wg_sweeps else None
     el_max = elapsed
+    el_ranks = [elapsed]
+    dist_world = 1
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev if args.dist_backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el_max = float(t.item())
+        el_ranks = [None] * world
+        dist.all_gather_object(el_ranks, elapsed)
+        dist_world = dist.get_world_size()
 
     if rank == 0:
         value = world * B * args.steps / el_max
@@ -385,6 +487,8 @@ def main():
             "value": value,
             "unit": "env-steps/s",
             "n_gpus": world,
+            "dist_world_size": dist_world,
+            "per_rank_value": [B * args.steps / e for e in el_ranks],
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": el_max / args.steps * 1e3,
