@@ -213,11 +213,6 @@ def kernel_name(N, part=0):
     groups of `part` oscillators per workgroup when N > 1024)."""
     if N > 1024:
         return f"kura_step_kernel<{(part or 1024) // 256}, true>"
-    kern = os.environ.get("KURA_KERNEL", "k1")
-    if kern == "k1t":    # team-overlapped solver (round 3 experiment, A/B)
-        return f"kura_stept_kernel<{N // 256}>"
-    if kern == "k1w":    # one wave per SIMD (round 3 experiment, A/B)
-        return f"kura_step1w_kernel<{N // 128}, false>"
     return f"kura_step_kernel<{N // 256}, false>"
 
 

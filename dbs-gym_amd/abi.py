@@ -26,7 +26,7 @@ FLAG_NAMES = {
     KURA_F_MAX_STEPS: "The maximum number of solver steps was reached",   # diffrax's message (throw=True)
     KURA_F_NONFINITE: "non-finite (NaN/Inf) state or RHS",
     KURA_F_GRID: "save grid outside [2, KURA_S_MAX] samples",
-    KURA_F_BARRIER: "split-group barrier (or K1t team wait) timed out",
+    KURA_F_BARRIER: "split-group barrier timed out",
     KURA_F_BOUNDS: "device access outside its buffer (KURA_DEBUG build)",
 }
 
@@ -92,6 +92,11 @@ class KuraConfig(ctypes.Structure):
     ]
 
 
+# exported by the KURA_DEBUG build (libkura_debug.so) only
+_DEBUG_SYMBOLS = {
+    "kura_debug_read_workspace": (c_int, [c_void_p, c_void_p, c_int64]),
+}
+
 _SYMBOLS = {
     # name: (restype, argtypes)
     "kura_create": (c_int, [POINTER(KuraConfig), c_int, POINTER(c_void_p)]),
@@ -107,7 +112,6 @@ _SYMBOLS = {
     "kura_reward": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p]),
     "kura_reward_n": (c_int, [c_void_p, c_int, c_void_p, c_int64, c_int64, c_int, c_void_p, c_void_p, c_int,
                               c_void_p, c_void_p, c_void_p]),
-    "kura_debug_read_workspace": (c_int, [c_void_p, c_void_p, c_int64]),
     "kura_get_state": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "kura_set_state": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "kura_set_env_gain": (c_int, [c_void_p, c_int, c_int, c_void_p]),
@@ -145,6 +149,11 @@ def load_library(path: str | None = None) -> ctypes.CDLL:
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    for name, (res, args) in _DEBUG_SYMBOLS.items():
+        if hasattr(lib, name):
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
     if lib.kura_abi_version() != KURA_ABI_VERSION:
         raise RuntimeError("libkura ABI version mismatch")
     if path is None:

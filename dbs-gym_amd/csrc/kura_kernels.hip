@@ -105,7 +105,6 @@ struct DevParams {
     int episode_cap;
     float* ep_lfp;          // [B][episode_cap] theta_mean samples of the running episode
     int* ep_len;            // [B] samples appended since the env's last reset
-    int desync_cycles;      // odd workgroups start this many cycles late (spreads record bursts)
     int* eflags;            // [B] per-env failure bits of the last launch (KURA_F_*, kura.h), 0 = ok
     float* rows;            // optional [B][KURA_S_MAX+1][N]: every saved row of a step (sol_state_, env.py:430,440)
 };
@@ -225,13 +224,12 @@ __device__ __forceinline__ T* uniform_ptr(T* ptr) {
 }
 
 
-// NWV: waves of the workgroup (8 for K1/K2, 4 for the one-wave-per-SIMD K1w/K2w
-// of kura_k1w.inc); wave w owns column tiles w*TPW .. w*TPW+TPW-1 either way.
-template <int TPW, int NWV = NWAVES>
+// wave w owns column tiles w*TPW .. w*TPW+TPW-1
+template <int TPW>
 __device__ __forceinline__ void coupling_gemm(const float* __restrict__ Xs, const float* __restrict__ alpha_sw,
                                               floatx16 (&acc)[TPW], unsigned long long* dbg = nullptr) {
     (void)dbg;  // KURA_DEBUG: bounds flag target
-    constexpr int N = TPW * 32 * NWV;
+    constexpr int N = TPW * 32 * NWAVES;
     constexpr int NK8 = N / 8;
     constexpr int TSTRIDE = NK8 * 64;  // floatx4 per column tile
     // lane id re-derived here (volatile: never CSE'd with a long-lived value),
@@ -432,10 +430,6 @@ struct CtlE {
     int keep, nsave;          // decision of the last attempted step
     int acc_steps, acc_rej;   // over the solves of one launch (stats)
     float t1, tprev, tnext, h, dtn;
-    // K1w (kura_k1w.inc) decides and advances time before the saves of the
-    // step: the save pass reads the step's own save index and interval here
-    int sv_si;
-    float sv_tprev, sv_tnext;
 };
 __shared__ CtlE s_ctl[E_WG];
 __shared__ float s_kn[E_WG];  // per-env coupling gain of the workgroup's envs
@@ -1464,8 +1458,6 @@ __device__ void solve_wg(const DevParams& __restrict__ p, float* Xs, int env_bas
     *rhs_count += nrhs;
 }
 
-#include "kura_k1t.inc"
-
 __device__ __forceinline__ void flush_stats(const DevParams& p, long long rhs, int env_base) {
     if (threadIdx.x != 0) return;
     unsigned long long steps = 0, rej = 0, flags = 0;
@@ -1852,21 +1844,13 @@ __device__ void r2_filters_wg(const DevParams& p, int env_base, double (&out)[EN
 // Launch-wide failure bits an env inherits: a split-group barrier that timed
 // out (group_barrier) leaves every later exchange of the launch unsynchronised.
 __device__ __forceinline__ int launch_flags(const DevParams& p, bool xl) {
-    if (!xl) return 0;  // (xl: split groups, or K1t's team waits -- both can time out)
+    if (!xl) return 0;  // split groups only: their group barriers can time out
     const unsigned long long v = __hip_atomic_load((__attribute__((address_space(1))) unsigned long long*)&p.stats[3],
                                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return (int)(v & KURA_F_BARRIER);
 }
 
-// the workgroup solver of a step / reset: K1's solve_wg, or K1t's solve_t (TEAM)
-template <int TPW, bool XL, bool TEAM>
-__device__ __forceinline__ void solve_sel(const DevParams& __restrict__ p, float* Xs, int env_base, bool to_ring,
-                                          bool pulse_on, long long* rhs, Part& pt) {
-    if constexpr (TEAM) solve_t<TPW>(p, Xs, env_base, to_ring, pulse_on, rhs, pt);
-    else solve_wg<TPW, XL>(p, Xs, env_base, to_ring, pulse_on, rhs, pt);
-}
-
-template <int TPW, bool XL, bool TEAM = false>
+template <int TPW, bool XL>
 __device__ __forceinline__ void step_pair(const DevParams& p, Part& pt, float* Xs, const float* __restrict__ action,
                                           float* __restrict__ obs, double* __restrict__ reward,
                                           uint8_t* __restrict__ done, float* __restrict__ lfp_true,
@@ -1876,12 +1860,6 @@ __device__ __forceinline__ void step_pair(const DevParams& p, Part& pt, float* X
     const int env_base = pt.group * E_WG;
     const int c0 = XL ? pt.col0 : 0, c1 = XL ? pt.col0 + TPW * 256 : N;   // oscillators of this workgroup
     __syncthreads();  // previous pair's LDS readers
-    if (!XL && p.desync_cycles > 0 && (blockIdx.x & 1)) {
-        // every workgroup runs the same phase sequence, so without an offset
-        // all CUs hit the record traffic of a stage input at the same time
-        const unsigned long long t0 = __builtin_amdgcn_s_memtime();
-        while (__builtin_amdgcn_s_memtime() - t0 < (unsigned long long)p.desync_cycles) __builtin_amdgcn_s_sleep(8);
-    }
     ctl_clear();
     // ---- thread e: rescale_action (env.py:389-393), ON grid (env.py:426-428)
     if (tid < E_WG) {
@@ -1920,7 +1898,7 @@ __device__ __forceinline__ void step_pair(const DevParams& p, Part& pt, float* X
     }
     __syncthreads();
     long long rhs = 0;
-    solve_sel<TPW, XL, TEAM>(p, Xs, env_base, false, true, &rhs, pt);
+    solve_wg<TPW, XL>(p, Xs, env_base, false, true, &rhs, pt);
     __syncthreads();  // global stores of the solve (y) before the OFF setup
     // ---- stimulation OFF (env.py:433-441)
     if (tid < E_WG) {
@@ -1943,7 +1921,7 @@ __device__ __forceinline__ void step_pair(const DevParams& p, Part& pt, float* X
         }
     }
     __syncthreads();
-    solve_sel<TPW, XL, TEAM>(p, Xs, env_base, false, false, &rhs, pt);
+    solve_wg<TPW, XL>(p, Xs, env_base, false, false, &rhs, pt);
     STAMP_DECL  // diagnostic build: the tail's phases in slots 20-22
     __syncthreads();
     // ---- window, reward, outputs (env.py:443-454): wave w owns envs 2w, 2w+1
@@ -1965,7 +1943,7 @@ __device__ __forceinline__ void step_pair(const DevParams& p, Part& pt, float* X
             const int e = wave * ENVS_PER_WAVE + ee;
             const int env = env_base + e;
             const int S = s_nI[e] + s_nII[e] - 1;
-            oks[ee] = env < p.B && !(s_ctl[e].flags | launch_flags(p, XL || TEAM)) && S >= 1;
+            oks[ee] = env < p.B && !(s_ctl[e].flags | launch_flags(p, XL)) && S >= 1;
             xvs[ee] = WinView{p.ring + (size_t)(oks[ee] ? env : 0) * p.W, e, p.W, oks[ee] ? p.wpos[env] : 0, S};
         }
         bbpow_multi<ENVS_PER_WAVE>(p, xvs, oks, bbv);
@@ -1978,7 +1956,7 @@ __device__ __forceinline__ void step_pair(const DevParams& p, Part& pt, float* X
         if (env >= p.B) continue;
         const CtlE& c = s_ctl[e];
         const int S = s_nI[e] + s_nII[e] - 1;
-        const int fl = c.flags | launch_flags(p, XL || TEAM);
+        const int fl = c.flags | launch_flags(p, XL);
         if (lane == 0) p.eflags[env] = fl;
         if (fl || S < 1) {
             // failed step (kura.h KURA_F_*): no state advance, done = 1; the
@@ -2068,7 +2046,7 @@ __global__ __launch_bounds__(NTHREADS) void kura_step_kernel(DevParams p, const 
 }
 
 // ----------------------------------------------------------- reset kernel --
-template <int TPW, bool XL, bool TEAM = false>
+template <int TPW, bool XL>
 __device__ __forceinline__ void reset_pair(const DevParams& p, Part& pt, float* Xs, const uint8_t* __restrict__ mask,
                                            const float* __restrict__ theta0, float* __restrict__ obs) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, tid = threadIdx.x;
@@ -2093,7 +2071,7 @@ __device__ __forceinline__ void reset_pair(const DevParams& p, Part& pt, float* 
     }
     __syncthreads();
     long long rhs = 0;
-    solve_sel<TPW, XL, TEAM>(p, Xs, env_base, true, false, &rhs, pt);
+    solve_wg<TPW, XL>(p, Xs, env_base, true, false, &rhs, pt);
     __syncthreads();  // ring rows written by thread e are read by every lane below
 #pragma unroll 1
     for (int ee = 0; ee < ((!XL || pt.part == 0) ? ENVS_PER_WAVE : 0); ++ee) {
@@ -2101,7 +2079,7 @@ __device__ __forceinline__ void reset_pair(const DevParams& p, Part& pt, float* 
         const int env = env_base + e;
         if (env >= p.B || (mask && !mask[env])) continue;
         if (lane == 0) {
-            p.eflags[env] = s_ctl[e].flags | launch_flags(p, XL || TEAM);
+            p.eflags[env] = s_ctl[e].flags | launch_flags(p, XL);
             p.t[env] = grid_at_c(s_ctl[e], s_ctl[e].n - 1);
             p.step[env] = 0;
             p.wpos[env] = 0;
@@ -2128,25 +2106,6 @@ __global__ __launch_bounds__(NTHREADS) void kura_reset_kernel(DevParams p, const
         Part pt = make_part(p, blockIdx.x);
         reset_pair<TPW, XL>(p, pt, Xs, mask, theta0, obs);
     }
-}
-
-// K1t / K2t (kura_k1t.inc): K1's step / reset with the team-overlapped solver
-template <int TPW>
-__global__ __launch_bounds__(NTHREADS) void kura_stept_kernel(DevParams p, const float* __restrict__ action,
-                                                              float* __restrict__ obs, double* __restrict__ reward,
-                                                              uint8_t* __restrict__ done, float* __restrict__ lfp_true,
-                                                              double* __restrict__ lfp_rec, int* __restrict__ nsamp) {
-    extern __shared__ float Xs[];
-    Part pt = make_part(p, blockIdx.x);
-    step_pair<TPW, false, true>(p, pt, Xs, action, obs, reward, done, lfp_true, lfp_rec, nsamp);
-}
-template <int TPW>
-__global__ __launch_bounds__(NTHREADS) void kura_resett_kernel(DevParams p, const uint8_t* __restrict__ mask,
-                                                               const float* __restrict__ theta0,
-                                                               float* __restrict__ obs) {
-    extern __shared__ float Xs[];
-    Part pt = make_part(p, blockIdx.x);
-    reset_pair<TPW, false, true>(p, pt, Xs, mask, theta0, obs);
 }
 
 // ------------------------------------------------------ standalone reward --
@@ -2220,7 +2179,6 @@ __global__ __launch_bounds__(64) void kura_reward_n_kernel(DevParams p, const do
     if (lane == 0) out[j] = r;
 }
 
-#include "kura_k1w.inc"
 #include "kura_fft.inc"
 
 // ------------------------------------------------------------- self-tests --

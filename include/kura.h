@@ -65,9 +65,8 @@ enum {
     KURA_F_MAX_STEPS = 1,   /* diffeqsolve max_steps reached */
     KURA_F_NONFINITE = 2,   /* NaN/Inf state or RHS (non-finite error norm) */
     KURA_F_GRID = 8,        /* save grid outside [2, KURA_S_MAX] samples */
-    KURA_F_BARRIER = 16,    /* split-group (N > 1024) barrier, or a K1t team
-                               wait, timed out: every exchange after it is
-                               unsynchronised */
+    KURA_F_BARRIER = 16,    /* split-group (N > 1024) barrier timed out: every
+                               exchange after it is unsynchronised */
     KURA_F_BOUNDS = 32      /* KURA_DEBUG builds (libkura_debug.so) only: a
                                record / alpha / ring / sample access outside
                                its buffer (kura_get_stats()[3]) */
@@ -203,10 +202,13 @@ int kura_get_state(KuraHandle* h, float* y /* B*N */, double* t /* B */, int32_t
                    double* ring /* B*W */, int32_t* wpos /* B */);
 int kura_set_state(KuraHandle* h, const float* y, const double* t, const int32_t* step,
                    const double* ring, const int32_t* wpos);
-/* diagnostic: copy the solver workspace (records, [B_pad/16][14][N][16]
- * float32, B_pad = B rounded up to 16; syncs) to the host -- used to compare
- * kernel generations record by record (tools/record_probe.py) */
+#ifdef KURA_DEBUG
+/* KURA_DEBUG builds (libkura_debug.so) only, not exported by libkura.so:
+ * copy the solver workspace (records, [B_pad/16][14][N][16] float32, B_pad =
+ * B rounded up to 16; syncs) to the host -- used to compare kernel
+ * generations record by record (tools/record_probe.py) */
 int kura_debug_read_workspace(KuraHandle* h, float* out, int64_t n);
+#endif
 /* optional capture of every saved phase row of each kura_step: rows_dev
  * (device, B*(KURA_S_MAX+1)*N float32, or NULL to stop) receives, per env,
  * rows 0 .. S of the step -- ys_I then ys_II, the reference's sol_state_

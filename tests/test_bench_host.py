@@ -33,16 +33,10 @@ def test_part_width_reaches_the_config():
             sim.make_config(p, 32, reward_func="bbpow_action", part_osc=bad)
 
 
-def test_bench_kernel_name(monkeypatch):
+def test_bench_kernel_name():
     bench = importlib.import_module("bench")
-    monkeypatch.delenv("KURA_KERNEL", raising=False)
-    assert bench.kernel_name(1024) == "kura_step_kernel<4, false>"       # K1 (default)
+    assert bench.kernel_name(1024) == "kura_step_kernel<4, false>"
     assert bench.kernel_name(512) == "kura_step_kernel<2, false>"
-    monkeypatch.setenv("KURA_KERNEL", "k1t")                              # team-overlapped (A/B)
-    assert bench.kernel_name(1024) == "kura_stept_kernel<4>"
-    monkeypatch.setenv("KURA_KERNEL", "k1w")                              # one wave per SIMD (A/B)
-    assert bench.kernel_name(1024) == "kura_step1w_kernel<8, false>"
-    monkeypatch.delenv("KURA_KERNEL")
     assert bench.kernel_name(8192) == "kura_step_kernel<4, true>"
     assert bench.kernel_name(8192, 256) == "kura_step_kernel<1, true>"
     assert bench.kernel_name(8192, 512) == "kura_step_kernel<2, true>"

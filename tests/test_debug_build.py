@@ -1,8 +1,8 @@
 """The KURA_DEBUG build (libkura_debug.so, __graft_entry__.build()): device
 bounds checks on every solver record, alpha fragment, ring row and LFP sample
 access (kura_kernels.hip KDBG_CHECK).  A violation raises KURA_F_BOUNDS in
-kura_get_stats()[3].  The GPU tests run the production kernels (K1, K1t, the
-N > 1024 split groups) under it, bit-exact against the oracle, and require
+kura_get_stats()[3].  The GPU tests run the production kernels (K1 and the
+N > 1024 split groups, incl. the persistent pair loop) under it, bit-exact against the oracle, and require
 that no access was out of bounds (the tool that names a
 faulting or silently-zero raw buffer access)."""
 import ctypes
@@ -22,24 +22,25 @@ def test_debug_library_exports_every_symbol():
     if not os.path.exists(DEBUG_LIB):
         pytest.skip("libkura_debug.so not built")
     lib = ctypes.CDLL(DEBUG_LIB)
-    for name in abi._SYMBOLS:
+    for name in (*abi._SYMBOLS, *abi._DEBUG_SYMBOLS):
         assert hasattr(lib, name), name
     assert lib.kura_abi_version() == abi.KURA_ABI_VERSION
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("kernel,name,n_osc,reward", [
-    ("k1", "env1", 1024, "bbpow_action"),
-    ("k1", "env0", 512, "temp_const_action"),
-    ("k1t", "env1", 1024, "bbpow_action"),
-    ("k1", "env0", 2048, "bbpow_action"),     # split groups (XL)
+@pytest.mark.parametrize("name,n_osc,reward,max_grid", [
+    ("env1", 1024, "bbpow_action", None),
+    ("env0", 512, "temp_const_action", None),
+    ("env0", 2048, "bbpow_action", None),     # split groups (XL)
+    ("env1", 2048, "temp_const_action", "2"),  # XL persistent pair loop: 2 groups x 2 parts on a grid of 2
 ])
-def test_debug_build_in_bounds_and_bit_exact(monkeypatch, kernel, name, n_osc, reward):
+def test_debug_build_in_bounds_and_bit_exact(monkeypatch, name, n_osc, reward, max_grid):
     torch = pytest.importorskip("torch")
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     assert os.path.exists(DEBUG_LIB), "libkura_debug.so missing: run __graft_entry__.build()"
-    monkeypatch.setenv("KURA_KERNEL", kernel)
+    if max_grid:   # debug-build hook: cap the co-resident split-group grid
+        monkeypatch.setenv("KURA_XL_MAX_GRID", max_grid)
     sim_mod = importlib.import_module("dbs-gym_amd.sim")
     B = 20
     cfg, alpha, omega, gs, gr, th0, ct, st, _ = make_case(name, n_osc, B, reward=reward)

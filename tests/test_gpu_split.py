@@ -22,11 +22,15 @@ def torch_gpu():
     return torch
 
 
-def _pair(torch, N, B, steps, reward="bbpow_action", name="env0", gains=None, part=0):
+DEBUG_LIB = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "dbs-gym_amd", "csrc",
+                         "libkura_debug.so")
+
+
+def _pair(torch, N, B, steps, reward="bbpow_action", name="env0", gains=None, part=0, lib=None):
     sim_mod = importlib.import_module("dbs-gym_amd.sim")
     cfg, alpha, omega, gs, gr, th0, ct, st, _ = make_case(name, N, B, reward=reward)
     cfg.part_osc = part
-    sim = sim_mod.KuraSim(cfg, 0)
+    sim = sim_mod.KuraSim(cfg, 0, lib_path=lib)
     sim.set_coupling(alpha)
     sim.set_env_params(omega, gs, gr)
     sim.set_spectral(ct, st)
@@ -65,9 +69,10 @@ def test_split_n4096_env1_random_gain(torch_gpu):
 
 
 def test_split_persistent_pair_loop(torch_gpu, monkeypatch):
-    """Grid capped below the number of (group, part) pairs: workgroups loop."""
+    """Grid capped below the number of (group, part) pairs: workgroups loop.
+    (The cap is a test hook of the KURA_DEBUG build, libkura_debug.so.)"""
     monkeypatch.setenv("KURA_XL_MAX_GRID", "4")
-    _pair(torch_gpu, 2048, 40, 2)          # 3 groups x 2 parts on a grid of 4
+    _pair(torch_gpu, 2048, 40, 2, lib=DEBUG_LIB)          # 3 groups x 2 parts on a grid of 4
 
 
 def test_split_n8192_stress_config(torch_gpu):

@@ -1,8 +1,6 @@
 #!/usr/bin/env python3
 """Diagnostic: per-phase cycle breakdown of the step kernel (KURA_STAMPS build;
-KURA_KERNEL=k1t (default) | k1 | k1w selects the kernel; K1t reuses K1's phase
-slots: gemm = both GEMM halves, barrier1 = the team waits before them,
-barrier2 = the pass's WAR wait or the step-end barrier; slot 19 = 1 + SIMD id).
+slot 19 = 1 + SIMD id).
 
 Builds dbs-gym_amd/csrc/libkura_stamps.so with -DKURA_STAMPS and runs a few
 bench-shaped steps, printing the share of wave cycles in each phase."""
@@ -18,12 +16,6 @@ import __graft_entry__ as ge  # noqa: E402
 
 SI = os.environ.get("SI") == "1"  # stage-input sub-phases (KURA_STAMPS_SI build, no record prefetch)
 LIB = os.path.join(ge.CSRC, "libkura_stamps_si.so" if SI else "libkura_stamps.so")
-KERN = os.environ.get("KURA_KERNEL", "k1")
-K1W = KERN == "k1w"
-# K1w (kura_k1w.inc) reuses the slots with its own phase names
-PHASES_W1 = ["stage_pass", "barrier_pre_gemm", "gemm", "-", "barrier_post_gemm", "last_pass", "err_barrier",
-             "decide", "saves", "fsal", "outside_solve", "reward_tail", "-", "-", "-", "-", "-", "-", "-", "-",
-             "-", "-", "-", "-"]
 PHASES = ["stage_input", "barrier1", "gemm", "epilogue", "barrier2", "post_err", "flag_sync", "post_decide",
           "post_saves", "post_fsal", "post_time", "save_setup", "save_loadwait", "save_compute", "save_publish",
           "save_totals", "si_load", "si_compute", "si_lds", "si_misc", "tail_window", "tail_reward", "tail_other",
@@ -73,8 +65,8 @@ def main():
         ev_ms = ms_reset
     else:
         ev_ms = ev0.elapsed_time(ev1) / nsteps
-    names = PHASES_W1 if K1W else PHASES
-    nwaves = 4 if K1W else 8
+    names = PHASES
+    nwaves = 8
     s = s[:nwaves]
     tot = s.sum(axis=1, keepdims=True)
     share = (s / np.maximum(tot, 1)).mean(axis=0)
