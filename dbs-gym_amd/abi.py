@@ -114,6 +114,8 @@ _SYMBOLS = {
                               c_void_p, c_void_p, c_void_p]),
     "kura_get_state": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "kura_set_state": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "kura_get_spec": (c_int, [c_void_p, c_void_p]),
+    "kura_set_spec": (c_int, [c_void_p, c_void_p]),
     "kura_set_env_gain": (c_int, [c_void_p, c_int, c_int, c_void_p]),
     "kura_psd_bbpow": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int, c_double, c_double, c_double, c_void_p,
                                c_void_p]),

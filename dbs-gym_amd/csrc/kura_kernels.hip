@@ -88,7 +88,8 @@ struct DevParams {
     int* wpos;              // [B] next write slot == oldest sample
     float* R;               // [B/16][NSLOT][N][16] solver workspace: per slot, 16 envs per oscillator
     float* pulse;           // [B][N]
-    double* scratch;        // [B][W + 2*padlen] * 2 (R2 filtfilt)
+    const double* r2c;      // [W] R2 filter functional c: filtfilt(x)[-1] - mean = c . x (kura_r2.h)
+    double* spec;           // [B][2 n_bins] R1/R3 spectral accumulators (re, im per bin; spec_step)
     unsigned long long* stats;  // [KURA_NSTATS] (kura.h)
     unsigned long long* stamps; // [NWAVES][KURA_NSTAMP] phase cycle counters (KURA_STAMPS builds only)
     // split groups (N > 1024): npart workgroups share an env group, each owns
@@ -1503,8 +1504,9 @@ __device__ __forceinline__ double window_dot(const double (&x)[WPL], const doubl
     return wave_sum_f64(a);
 }
 
-// Window accessor for the serial filter: x[i] (oldest first) is either an
-// untouched slot of the ring or one of the S new samples held in LDS.
+// Window accessor: x[i] (oldest first) of the window after this step's
+// append is either an untouched slot of the ring or one of the S new samples
+// held in LDS.
 struct WinView {
     const double* ring;
     int e;
@@ -1520,115 +1522,19 @@ struct WinView {
     }
 };
 
-// R2 = -1e3 (filtfilt(x)[-1] - mean(filtfilt(x)))^2 - 1e-2|u0|: scipy
-// filtfilt (odd extension of padlen samples, DF2T lfilter with lfilter_zi
-// scaled by each pass's first input), oracle filtfilt_last.  Called by the
-// whole wave.  The recursion is serial, so it walks 64 samples at a time:
-// the block is loaded lane-parallel, each sample is taken in order with
-// readlane (the filter state is wave-uniform), the outputs are gathered with
-// a lane select and stored lane-parallel -- the same operations in the same
-// order as the oracle, without a memory round trip per sample.  The mean is
-// the R64 reduction (lane partials in index order, xor butterfly).
-__device__ __forceinline__ double readlane_f64(double v, int j) {
-    const uint64_t u = __builtin_bit_cast(uint64_t, v);
-    const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)u, j);
-    const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(u >> 32), j);
-    return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
-}
-// NF independent windows at once (two envs of a wave): their recursions are
-// interleaved in one loop, which is bound by the latency of the dependent
-// f64 chain, not by issue.
-template <int NF>
-__device__ void filtfilt_last_wave(const DevParams& p, const WinView (&xv)[NF], double* const (&ext)[NF],
-                                   double* const (&tmp)[NF], double (&out)[NF]) {
-    const int lane = threadIdx.x & 63;
-    const int W = p.W, P = p.padlen, L = W + 2 * P;
-#pragma unroll
-    for (int f = 0; f < NF; ++f) {
-        const double x0 = xv[f].at(0), xl = xv[f].at(W - 1);
-        for (int k = lane; k < L; k += 64) {
-            double v;
-            if (k < P) v = 2.0 * x0 - xv[f].at(P - k);
-            else if (k < P + W) v = xv[f].at(k - P);
-            else v = 2.0 * xl - xv[f].at(W - 2 - (k - P - W));
-            ext[f][k] = v;
-        }
-    }
-    __threadfence_block();  // this wave's stores before its lanes read each other's elements
-    const double b0 = p.bw_b[0], b1 = p.bw_b[1], b2 = p.bw_b[2], b3 = p.bw_b[3], b4 = p.bw_b[4];
-    const double a1 = p.bw_a[1], a2 = p.bw_a[2], a3 = p.bw_a[3], a4 = p.bw_a[4];
-    for (int pass = 0; pass < 2; ++pass) {
-        double z0[NF], z1[NF], z2[NF], z3[NF];
-#pragma unroll
-        for (int f = 0; f < NF; ++f) {
-            const double e0 = ext[f][0];
-            z0[f] = p.bw_zi[0] * e0;
-            z1[f] = p.bw_zi[1] * e0;
-            z2[f] = p.bw_zi[2] * e0;
-            z3[f] = p.bw_zi[3] * e0;
-        }
-        for (int k0 = 0; k0 < L; k0 += 64) {
-            const int nb = L - k0 < 64 ? L - k0 : 64;
-            double vin[NF], vout[NF];
-#pragma unroll
-            for (int f = 0; f < NF; ++f) {
-                vin[f] = k0 + lane < L ? ext[f][k0 + lane] : 0.0;
-                vout[f] = 0.0;
-            }
-            for (int j = 0; j < nb; ++j) {
-#pragma unroll
-                for (int f = 0; f < NF; ++f) {
-                    const double xn = readlane_f64(vin[f], j);
-                    const double yn = z0[f] + b0 * xn;
-                    z0[f] = (z1[f] + xn * b1) - yn * a1;
-                    z1[f] = (z2[f] + xn * b2) - yn * a2;
-                    z2[f] = (z3[f] + xn * b3) - yn * a3;
-                    z3[f] = xn * b4 - yn * a4;
-                    vout[f] = lane == j ? yn : vout[f];
-                }
-            }
-#pragma unroll
-            for (int f = 0; f < NF; ++f)
-                if (k0 + lane < L) tmp[f][k0 + lane] = vout[f];
-        }
-        __threadfence_block();
-        if (pass == 0) {
-#pragma unroll
-            for (int f = 0; f < NF; ++f)
-                for (int k = lane; k < L; k += 64) ext[f][k] = tmp[f][L - 1 - k];
-            __threadfence_block();
-        }
-    }
-    // filtered window g[i] = tmp[L-1-P-i], i < W; g[W-1] = tmp[P]
-#pragma unroll
-    for (int f = 0; f < NF; ++f) {
-        double part = 0.0;
-        for (int i = lane; i < W; i += 64) part = part + tmp[f][L - 1 - P - i];
-        const double mean = wave_sum_f64(part) / (double)W;
-        out[f] = tmp[f][P] - mean;
-    }
-}
-
-// Reward of the window held in registers (R64 layout), env.py:638-688.
-// Must be called by the whole wave (the DFT reductions shuffle).
-// PRE: the R2 filter term d is given (*d_pre, the step kernels' r2_filters);
-// otherwise it is computed here (the standalone reward kernel).
-template <int WPL, bool PRE = false>
-__device__ __forceinline__ double reward_of(const DevParams& p, const double (&x)[WPL], double u0, const WinView& xv,
-                                            double* ext, double* tmp, const double* d_pre = nullptr) {
+// Reward of the window held in registers (R64 layout), env.py:638-688 (the
+// standalone reward kernel).  Must be called by the whole wave.
+//   R1 / R3: the 10 beta bins as float64 DFT dots (calc_beta_band_power,
+//            utils.py:21-27);
+//   R2:      d = c . x, the filtfilt term as a linear functional (kura_r2.h:
+//            f[-1] - mean(f) of scipy's filtfilt is linear in the window).
+template <int WPL>
+__device__ __forceinline__ double reward_of(const DevParams& p, const double (&x)[WPL], double u0) {
     const double au = fabs(u0);
     if (p.reward_kind == KURA_R_TEMP_CONST) {
-        double d[1];
-        if (PRE) {
-            d[0] = *d_pre;
-        } else {
-            const WinView v1[1] = {xv};
-            double* const e1[1] = {ext};
-            double* const t1[1] = {tmp};
-            filtfilt_last_wave<1>(p, v1, e1, t1, d);
-        }
-        const double r1 = 1e3 * (d[0] * d[0]);
-        return __shfl(-r1 - 1e-2 * au, 0, 64);
+        const double d = window_dot<WPL>(x, p.r2c, p.W);
+        const double r1 = 1e3 * (d * d);
+        return -r1 - 1e-2 * au;
     }
     double bb = 0.0;
     for (int b = 0; b < p.n_bins; ++b) {
@@ -1649,68 +1555,114 @@ __device__ __forceinline__ double reward_of(const DevParams& p, const double (&x
 
 #define WPL_MAX 40  // ceil(W/64) upper bound supported (W <= 2560)
 
-// Beta-band power (calc_beta_band_power's sum over the bins, utils.py:21-27)
-// of the windows of NE envs of one wave at once, in the R64 order of
-// window_dot: lane l accumulates x[l + 64 m] * tab[l + 64 m] over m from +0,
-// then the xor butterfly; bins are added in index order from +0.  The bins
-// go in groups of BG (accumulators in registers); within a group every
-// twiddle element is loaded once for all NE envs (buffer loads through one
-// wave-uniform descriptor, 4 columns in flight), and the windows are read
-// straight from the ring / this step's samples (WinView).  ok[e] false:
-// bb[e] = 0 and nothing of env e is read.
-#define BB_G 5
+// R2's filter term d = c . x (kura_r2.h) of the windows of NE envs of one
+// wave at once, in the R64 order of window_dot (lane l accumulates
+// x[l + 64 m] * c[l + 64 m] over m from +0 by fma, then the xor butterfly):
+// one W-long dot per env in place of scipy's two serial filtfilt passes.  c
+// is read once per element for all NE envs (buffer loads through one
+// wave-uniform descriptor), the windows straight from the ring / this step's
+// samples (WinView).  ok[e] false: d[e] = 0 and nothing of env e is read.
 template <int NE>
-__device__ __forceinline__ void bbpow_multi(const DevParams& __restrict__ p, const WinView (&xv)[NE],
-                                            const bool (&ok)[NE], double (&bb)[NE]) {
+__device__ __forceinline__ void r2_dot_multi(const DevParams& __restrict__ p, const WinView (&xv)[NE],
+                                             const bool (&ok)[NE], double (&d)[NE]) {
+    const int lane = threadIdx.x & 63;
+    const int W = p.W;
+    const int nm = (W + 63) / 64;
+    const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc((void*)uniform_ptr(p.r2c), 0, W * 8,
+                                                                      0x00020000);
+    double acc[NE];
+#pragma unroll
+    for (int e = 0; e < NE; ++e) acc[e] = 0.0;
+#pragma unroll 4
+    for (int m = 0; m < nm; ++m) {
+        const int i = lane + 64 * m;
+        const bool valid = i < W;
+        const double c = __builtin_bit_cast(
+            double, __builtin_amdgcn_raw_buffer_load_b64(rc, valid ? i * 8 : 0x7FFFFFF0, 0, 0));  // out of range: 0
+#pragma unroll
+        for (int e = 0; e < NE; ++e) {
+            const double x = (valid && ok[e]) ? xv[e].at(i) : 0.0;
+            acc[e] = valid ? __builtin_fma(x, c, acc[e]) : acc[e];
+        }
+    }
+#pragma unroll
+    for (int e = 0; e < NE; ++e) d[e] = ok[e] ? wave_sum_f64(acc[e]) : 0.0;
+}
+
+// ---- R1 / R3 beta power from running spectral accumulators ---------------
+// calc_beta_band_power (utils.py:21-27) needs |X_k|^2 of the window's DFT at
+// the 10 in-band bins k.  With the window kept as a ring, X_k of the window
+// (oldest first) is e^{2 pi i k wpos / W} times Y_k = sum_p ring[p] e^{-2 pi i
+// k p / W}, the DFT over ring positions -- a pure phase, so |X_k| = |Y_k|.
+// Y_k changes only at the S slots a step overwrites:
+//     Y_k += (new - old) * (cos, -sin)(2 pi k p / W)    for each written slot p,
+// so each env keeps Y (spec[env][2 n_bins]: re, im per bin, float64) and a
+// step costs S * 2 n_bins fmas instead of 2 n_bins W-long dots.  The reset
+// (and kura_set_state / kura_set_spec) forms Y directly (spec_init, R64
+// order); the oracle keeps the same accumulators with the same operations
+// (oracle/kura_oracle.c spec_update), so the reward stays bit-exact, and it
+// agrees with the direct DFT to float64 rounding (~1e-14 relative over an
+// episode, tests/test_oracle_props.py).
+
+// whole wave: Y of env `env` from its ring (positions 0..W-1), R64 dots
+__device__ __forceinline__ void spec_init(const DevParams& __restrict__ p, int env) {
     const int lane = threadIdx.x & 63;
     const int W = p.W, nb = p.n_bins;
-    const int nm = (W + 63) / 64;
-    const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc((void*)uniform_ptr(p.ctab), 0, nb * W * 8,
-                                                                      0x00020000);
-    const __amdgpu_buffer_rsrc_t rsn = __builtin_amdgcn_make_buffer_rsrc((void*)uniform_ptr(p.stab), 0, nb * W * 8,
-                                                                       0x00020000);
-    auto ld = [&](const __amdgpu_buffer_rsrc_t& r, int off) {
-        return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
-    };
-#pragma unroll
-    for (int e = 0; e < NE; ++e) bb[e] = 0.0;
-#pragma unroll 1
-    for (int b0 = 0; b0 < nb; b0 += BB_G) {
-        double re[NE][BB_G], im[NE][BB_G];
-#pragma unroll
-        for (int e = 0; e < NE; ++e)
-#pragma unroll
-            for (int g = 0; g < BB_G; ++g) re[e][g] = im[e][g] = 0.0;
-#pragma unroll 4
-        for (int m = 0; m < nm; ++m) {
-            const int i = lane + 64 * m;
-            const bool valid = i < W;
-            double x[NE];
-#pragma unroll
-            for (int e = 0; e < NE; ++e) x[e] = (valid && ok[e]) ? xv[e].at(i) : 0.0;
-#pragma unroll
-            for (int g = 0; g < BB_G; ++g) {
-                if (b0 + g >= nb) break;  // wave-uniform
-                const int off = valid ? ((b0 + g) * W + i) * 8 : 0x7FFFFFF0;  // out of range: 0, unused
-                const double c = ld(rc, off), sn = ld(rsn, off);
-#pragma unroll
-                for (int e = 0; e < NE; ++e) {
-                    re[e][g] = valid ? __builtin_fma(x[e], c, re[e][g]) : re[e][g];
-                    im[e][g] = valid ? __builtin_fma(x[e], sn, im[e][g]) : im[e][g];
-                }
-            }
+    const double* rb = p.ring + (size_t)env * W;
+    double* sp = p.spec + (size_t)env * 2 * nb;
+    for (int b = 0; b < nb; ++b) {
+        double re = 0.0, im = 0.0;
+        for (int i = lane; i < W; i += 64) {
+            const double x = rb[i];
+            re = __builtin_fma(x, p.ctab[(size_t)b * W + i], re);
+            im = __builtin_fma(x, p.stab[(size_t)b * W + i], im);
         }
-#pragma unroll
-        for (int g = 0; g < BB_G; ++g) {
-            if (b0 + g >= nb) break;
-#pragma unroll
-            for (int e = 0; e < NE; ++e) {
-                const double pr = wave_sum_f64(re[e][g]) / (double)W, pi = wave_sum_f64(im[e][g]) / (double)W;
-                bb[e] = bb[e] + (pr * pr + pi * pi) * 2.0;
-            }
+        re = wave_sum_f64(re);
+        im = wave_sum_f64(im);
+        if (lane == 0) {
+            sp[2 * b] = re;
+            sp[2 * b + 1] = im;
         }
     }
 }
+
+// whole wave, before the ring append of env `env` (local env e): fold this
+// step's S samples (LDS s_smp_r[e]) into Y in sample order and return the
+// band power of the new window (the bins summed in index order from +0, as
+// calc_beta_band_power's np.sum does in the oracle).  Lane j < 2 n_bins owns
+// Y's component j (bin j/2, re or im) and walks the S slots in order.
+__device__ __forceinline__ double spec_step(const DevParams& __restrict__ p, int e, int env, int wp0, int S) {
+    const int lane = threadIdx.x & 63;
+    const int W = p.W, nb = p.n_bins;
+    // the values the S appends overwrite, read before any of them is stored
+    // (lane s; a slot written twice in one step, S > W, sees the first append)
+    double oldv = 0.0;
+    if (lane < S) {
+        int k = wp0 + lane;
+        while (k >= W) k -= W;
+        oldv = lane >= W ? s_smp_r[e][lane - W] : p.ring[(size_t)env * W + k];
+    }
+    double* sp = p.spec + (size_t)env * 2 * nb;
+    const bool own = lane < 2 * nb;
+    const double* tab = ((lane & 1) ? p.stab : p.ctab) + (size_t)(lane >> 1) * W;
+    double acc = own ? sp[lane] : 0.0;
+    int k = wp0;
+    for (int s = 0; s < S; ++s) {   // S is uniform over the wave
+        const double od = __shfl(oldv, s, 64);
+        const double dl = s_smp_r[e][s] - od;
+        if (own) acc = __builtin_fma(dl, tab[k], acc);
+        k = k + 1 == W ? 0 : k + 1;
+    }
+    if (own) sp[lane] = acc;
+    double bb = 0.0;
+    for (int b = 0; b < nb; ++b) {
+        const double re = __shfl(acc, 2 * b, 64), im = __shfl(acc, 2 * b + 1, 64);
+        const double pr = re / (double)W, pi = im / (double)W;
+        bb = bb + (pr * pr + pi * pi) * 2.0;
+    }
+    return bb;
+}
+
 // reward_of's closing expressions (env.py:638-688) from the band power bb (R1,
 // R3) or the filter term d (R2)
 __device__ __forceinline__ double reward_from(const DevParams& p, double bb, double d, double u0) {
@@ -1744,101 +1696,6 @@ __device__ __forceinline__ Part make_part(const DevParams& p, int pair) {
     pt.ep = 0;
     pt.xs_n = 0;
     return pt;
-}
-
-// R2 filters of the workgroup's envs (scipy filtfilt, oracle filtfilt_last),
-// same operations in the same order as filtfilt_last_wave:
-//  (A) each wave writes the odd-extended windows of its two envs to their
-//      scratch (lane-parallel);
-//  (B) wave 0 runs both recursion passes, lane e walking env e's sequence
-//      (16 chains per instruction stream instead of one), 16 samples per
-//      block of independent loads; pass 2 reads pass 1's output backwards;
-//  (C) each wave reduces the mean of its envs' filtered windows (R64 order).
-// Must be called by the whole workgroup; out[ee] = f[W-1] - mean(f) of env
-// 2*wave + ee (0 for envs without a reward).
-__device__ void r2_filters_wg(const DevParams& p, int env_base, double (&out)[ENVS_PER_WAVE]) {
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int W = p.W, P = p.padlen, L = W + 2 * P;
-    auto env_ok = [&](int e) {
-        const int env = env_base + e;
-        return env < p.B && !s_ctl[e].flags && (s_nI[e] + s_nII[e] - 1) >= 1;
-    };
-    auto ext_of = [&](int e) { return p.scratch + (size_t)(env_base + e) * 2 * (W + 2 * P); };
-    // (A)
-#pragma unroll 1
-    for (int ee = 0; ee < ENVS_PER_WAVE; ++ee) {
-        const int e = wave * ENVS_PER_WAVE + ee;
-        if (!env_ok(e)) continue;
-        const int env = env_base + e;
-        const WinView xv{p.ring + (size_t)env * W, e, W, p.wpos[env], s_nI[e] + s_nII[e] - 1};
-        double* ext = ext_of(e);
-        const double x0 = xv.at(0), xl = xv.at(W - 1);
-        for (int k = lane; k < L; k += 64) {
-            double v;
-            if (k < P) v = 2.0 * x0 - xv.at(P - k);
-            else if (k < P + W) v = xv.at(k - P);
-            else v = 2.0 * xl - xv.at(W - 2 - (k - P - W));
-            ext[k] = v;
-        }
-    }
-    __syncthreads();
-    // (B)
-    if (wave == 0 && lane < E_WG && env_ok(lane)) {
-        double* ext = ext_of(lane);
-        double* tmp = ext + L;
-        const double b0 = p.bw_b[0], b1 = p.bw_b[1], b2 = p.bw_b[2], b3 = p.bw_b[3], b4 = p.bw_b[4];
-        const double a1 = p.bw_a[1], a2 = p.bw_a[2], a3 = p.bw_a[3], a4 = p.bw_a[4];
-        for (int pass = 0; pass < 2; ++pass) {
-            // pass 0: ext -> tmp; pass 1: tmp read backwards -> ext
-            const double* src = pass == 0 ? ext : tmp;
-            double* dst = pass == 0 ? tmp : ext;
-            auto in = [&](int k) { return pass == 0 ? src[k] : src[L - 1 - k]; };
-            const double e0 = in(0);
-            double z0 = p.bw_zi[0] * e0, z1 = p.bw_zi[1] * e0, z2 = p.bw_zi[2] * e0, z3 = p.bw_zi[3] * e0;
-            auto sample = [&](double xn) {
-                const double yn = z0 + b0 * xn;
-                z0 = (z1 + xn * b1) - yn * a1;
-                z1 = (z2 + xn * b2) - yn * a2;
-                z2 = (z3 + xn * b3) - yn * a3;
-                z3 = xn * b4 - yn * a4;
-                return yn;
-            };
-            // full blocks of BLK samples, the next block's loads in flight
-            // while this block's recursion runs; then the tail
-            constexpr int BLK = 16;
-            const int nfull = L / BLK;
-            double xb[BLK];
-#pragma unroll
-            for (int i = 0; i < BLK; ++i) xb[i] = nfull > 0 ? in(i) : 0.0;
-#pragma unroll 1
-            for (int b = 0; b < nfull; ++b) {
-                const int k0 = b * BLK;
-                const bool more = b + 1 < nfull;
-                double xp[BLK];
-#pragma unroll
-                for (int i = 0; i < BLK; ++i) xp[i] = more ? in(k0 + BLK + i) : 0.0;
-#pragma unroll
-                for (int i = 0; i < BLK; ++i) dst[k0 + i] = sample(xb[i]);
-#pragma unroll
-                for (int i = 0; i < BLK; ++i) xb[i] = xp[i];
-            }
-#pragma unroll 1
-            for (int k = nfull * BLK; k < L; ++k) dst[k] = sample(in(k));
-        }
-    }
-    __syncthreads();
-    // (C) filtered window f[i] = y2[L-1-P-i] (y2 in ext), f[W-1] = y2[P]
-#pragma unroll
-    for (int ee = 0; ee < ENVS_PER_WAVE; ++ee) {
-        const int e = wave * ENVS_PER_WAVE + ee;
-        out[ee] = 0.0;
-        if (!env_ok(e)) continue;
-        const double* y2 = ext_of(e);
-        double part = 0.0;
-        for (int i = lane; i < W; i += 64) part = part + y2[L - 1 - P - i];
-        const double mean = wave_sum_f64(part) / (double)W;
-        out[ee] = y2[P] - mean;
-    }
 }
 
 // Launch-wide failure bits an env inherits: a split-group barrier that timed
@@ -1926,16 +1783,11 @@ __device__ __forceinline__ void step_pair(const DevParams& p, Part& pt, float* X
     __syncthreads();
     // ---- window, reward, outputs (env.py:443-454): wave w owns envs 2w, 2w+1
     // (split groups: part 0; every part holds the same samples)
-    // R2: the serial filters of all 16 envs of the workgroup run in one wave,
-    // one lane per env (r2_filters_wg), before the per-env loop (and so before
-    // the ring appends)
+    // R2: d = c . x of both envs of the wave at once (r2_dot_multi), before
+    // the ring appends below overwrite the window's oldest slots
     double r2d[ENVS_PER_WAVE] = {0.0, 0.0};
-    const bool r2 = p.reward_kind == KURA_R_TEMP_CONST && (!XL || pt.part == 0);
-    if (r2) r2_filters_wg(p, env_base, r2d);
-    // R1 / R3: beta-band power of both envs of the wave at once, before the
-    // ring appends below overwrite the window's oldest slots
-    double bbv[ENVS_PER_WAVE] = {0.0, 0.0};
-    if (!r2 && (!XL || pt.part == 0)) {
+    const bool r2 = p.reward_kind == KURA_R_TEMP_CONST;
+    if (r2 && (!XL || pt.part == 0)) {
         WinView xvs[ENVS_PER_WAVE];
         bool oks[ENVS_PER_WAVE];
 #pragma unroll
@@ -1946,7 +1798,7 @@ __device__ __forceinline__ void step_pair(const DevParams& p, Part& pt, float* X
             oks[ee] = env < p.B && !(s_ctl[e].flags | launch_flags(p, XL)) && S >= 1;
             xvs[ee] = WinView{p.ring + (size_t)(oks[ee] ? env : 0) * p.W, e, p.W, oks[ee] ? p.wpos[env] : 0, S};
         }
-        bbpow_multi<ENVS_PER_WAVE>(p, xvs, oks, bbv);
+        r2_dot_multi<ENVS_PER_WAVE>(p, xvs, oks, r2d);
     }
     STAMP(21);
 #pragma unroll 1
@@ -1979,7 +1831,10 @@ __device__ __forceinline__ void step_pair(const DevParams& p, Part& pt, float* X
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #endif
         STAMP(20);
-        const double r = reward_from(p, bbv[ee], r2d[ee], s_u[e][0]);
+        // R1 / R3: fold the S new samples into the env's spectral accumulators
+        // (old slot values read before the append below) -> band power
+        const double bb = r2 ? 0.0 : spec_step(p, e, env, wp0, S);
+        const double r = reward_from(p, bb, r2d[ee], s_u[e][0]);
         // ring append after every read of the old slots
         if (lane < S) {
             int k = wp0 + lane;
@@ -2087,8 +1942,16 @@ __device__ __forceinline__ void reset_pair(const DevParams& p, Part& pt, float* 
         }
         if (obs)
             for (int i = lane; i < W; i += 64) obs[(size_t)env * W + i] = (float)p.ring[(size_t)env * W + i];
+        // R1 / R3: the spectral accumulators of the new window (spec_step)
+        if (p.reward_kind != KURA_R_TEMP_CONST) spec_init(p, env);
     }
     if (!XL || pt.part == 0) flush_stats(p, rhs, env_base);
+}
+
+// kura_set_state / kura_set_spec(NULL) / kura_set_spectral: re-form every
+// env's spectral accumulators from its ring (one wave per env)
+__global__ __launch_bounds__(64) void kura_spec_init_kernel(DevParams p) {
+    if ((int)blockIdx.x < p.B) spec_init(p, blockIdx.x);
 }
 
 template <int TPW, bool XL>
@@ -2123,10 +1986,7 @@ __global__ __launch_bounds__(64) void kura_reward_kernel(DevParams p, const doub
         const int i = lane + 64 * m;
         x[m] = i < p.W ? xl[i] : 0.0;
     }
-    double* ext = p.scratch + (size_t)p.B * 2 * (p.W + 2 * p.padlen) + (size_t)env * 2 * (p.W + 2 * p.padlen);
-    double* tmp = ext + (p.W + 2 * p.padlen);
-    const WinView xv{xl, 0, p.W, 0, 0};
-    const double r = reward_of<WPL>(p, x, (double)u0[env], xv, ext, tmp);
+    const double r = reward_of<WPL>(p, x, (double)u0[env]);
     if (lane == 0) out[env] = r;
 }
 
@@ -2136,13 +1996,13 @@ __global__ __launch_bounds__(64) void kura_reward_kernel(DevParams p, const doub
 // samples PIDController.predict passes, aDBS_RL/agents/simple_dbs.py:81-88).
 // One wave per window, read from memory: R1/R3 = the bins' R64 dots against
 // host twiddle rows of length L (the same R64 order as window_dot, so a
-// length-W call equals kura_reward bit for bit), R2 = filtfilt_last_wave on
-// the window with p.W = L.
+// length-W call equals kura_reward bit for bit), R2 = the R64 dot with the
+// length-L functional c (kura_r2.h; the host caches one per length).
 __global__ __launch_bounds__(64) void kura_reward_n_kernel(DevParams p, const double* __restrict__ x, long long ld,
                                                            const double* __restrict__ ctab,
                                                            const double* __restrict__ stab, int n_bins,
                                                            const double* __restrict__ u0, double* __restrict__ out,
-                                                           double* __restrict__ scratch, int n) {
+                                                           const double* __restrict__ r2c, int n) {
     const int j = blockIdx.x;
     if (j >= n) return;
     const int lane = threadIdx.x;
@@ -2151,12 +2011,10 @@ __global__ __launch_bounds__(64) void kura_reward_n_kernel(DevParams p, const do
     const double au = fabs(u0[j]);  // float64: the caller's action as given (env.py:638-688)
     double r;
     if (p.reward_kind == KURA_R_TEMP_CONST) {
-        const WinView v1[1] = {WinView{xw, 0, L, 0, 0}};
-        double* const e1[1] = {scratch + (size_t)j * 2 * (L + 2 * p.padlen)};
-        double* const t1[1] = {e1[0] + (L + 2 * p.padlen)};
-        double d[1];
-        filtfilt_last_wave<1>(p, v1, e1, t1, d);
-        r = -(1e3 * (d[0] * d[0])) - 1e-2 * au;
+        double d = 0.0;
+        for (int i = lane; i < L; i += 64) d = __builtin_fma(xw[i], r2c[i], d);
+        d = wave_sum_f64(d);
+        r = -(1e3 * (d * d)) - 1e-2 * au;
     } else {
         double bb = 0.0;
         for (int b = 0; b < n_bins; ++b) {

@@ -278,6 +278,8 @@ class KuraSim:
         check(self.lib, self.lib.kura_get_state(self._h, st["y"].ctypes.data, st["t"].ctypes.data,
                                                 st["step"].ctypes.data, st["ring"].ctypes.data,
                                                 st["wpos"].ctypes.data), "kura_get_state")
+        st["spec"] = np.empty((B, 2 * self.cfg.n_bins), np.float64)   # R1/R3 spectral accumulators
+        check(self.lib, self.lib.kura_get_spec(self._h, st["spec"].ctypes.data), "kura_get_spec")
         return st
 
     def times(self) -> np.ndarray:
@@ -308,6 +310,11 @@ class KuraSim:
                 np.ascontiguousarray(st["step"], np.int32), np.ascontiguousarray(st["ring"], np.float64),
                 np.ascontiguousarray(st["wpos"], np.int32)]
         check(self.lib, self.lib.kura_set_state(self._h, *[a.ctypes.data for a in arrs]), "kura_set_state")
+        if "spec" in st:   # exact accumulators of a checkpoint (else re-formed from the ring)
+            sp = np.ascontiguousarray(st["spec"], np.float64)
+            if sp.shape != (self.B, 2 * self.cfg.n_bins):
+                raise ValueError(f"spec shape {sp.shape} != ({self.B}, {2 * self.cfg.n_bins})")
+            check(self.lib, self.lib.kura_set_spec(self._h, sp.ctypes.data), "kura_set_spec")
 
     def stats(self) -> np.ndarray:
         out = np.zeros(abi.KURA_NSTATS, np.int64)

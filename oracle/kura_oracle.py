@@ -39,9 +39,10 @@ def lib() -> ctypes.CDLL:
         L.oracle_create.argtypes = [c_void_p, c_void_p]
         L.oracle_destroy.argtypes = [c_void_p]
         L.oracle_reset.restype = c_int
-        L.oracle_reset.argtypes = [c_void_p, c_int] + [c_void_p] * 11
+        L.oracle_reset.argtypes = [c_void_p, c_int] + [c_void_p] * 14
         L.oracle_step.restype = c_int
-        L.oracle_step.argtypes = [c_void_p, c_int] + [c_void_p] * 19
+        L.oracle_step.argtypes = [c_void_p, c_int] + [c_void_p] * 20
+        L.oracle_spec_init.argtypes = [c_void_p, c_int] + [c_void_p] * 4
         L.oracle_solve_rows.restype = c_int
         L.oracle_solve_rows.argtypes = [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p]
         L.oracle_rhs.argtypes = [c_void_p] * 5
@@ -83,6 +84,7 @@ class Oracle:
         self.step_count = np.zeros(B, np.int32)
         self.ring = np.zeros((B, W), np.float64)
         self.wpos = np.zeros(B, np.int32)
+        self.spec = np.zeros((B, 2 * cfg.n_bins), np.float64)   # R1/R3 spectral accumulators
         self.stats = np.zeros(4, np.int64)
         self.flags = np.zeros(B, np.int32)   # KURA_F_* of the last reset/step per env
 
@@ -106,7 +108,8 @@ class Oracle:
         obs = np.zeros((self.B, self.W), np.float32)
         rc = lib().oracle_reset(self._ctx, self.B, _p(self.omega), _p(self.g_rec), _p(th), _p(self.y), _p(self.t),
                                 _p(self.step_count), _p(self.ring), _p(self.wpos), _p(obs), _p(self.stats),
-                                _p(self.flags))
+                                _p(self.flags), _p(getattr(self, "ctab", None)), _p(getattr(self, "stab", None)),
+                                _p(self.spec) if hasattr(self, "ctab") else None)
         assert rc == 0
         return obs
 
@@ -120,13 +123,27 @@ class Oracle:
                                _p(self.stab), _p(a), _p(self.y), _p(self.t), _p(self.step_count), _p(self.ring),
                                _p(self.wpos), _p(out["obs"]), _p(out["reward"]), _p(out["done"]),
                                _p(out["lfp_true"]), _p(out["lfp_rec"]), _p(out["nsamp"]), _p(self.stats),
-                               _p(self.flags))
+                               _p(self.flags), _p(self.spec))
         assert rc == 0
         return out
 
     def state(self):
         return dict(y=self.y.copy(), t=self.t.copy(), step=self.step_count.copy(), ring=self.ring.copy(),
-                    wpos=self.wpos.copy())
+                    wpos=self.wpos.copy(), spec=self.spec.copy())
+
+    def set_state(self, st):
+        """kura_set_state (+ kura_set_spec when st has 'spec'; else the
+        accumulators are re-formed from the ring, as the library does)."""
+        self.y[...] = st["y"]
+        self.t[...] = st["t"]
+        self.step_count[...] = st["step"]
+        self.ring[...] = st["ring"]
+        self.wpos[...] = st["wpos"]
+        if "spec" in st:
+            self.spec[...] = st["spec"]
+        elif self.cfg.reward_kind != 2 and self.cfg.n_bins:
+            lib().oracle_spec_init(ctypes.byref(self.cfg), self.B, _p(self.ring), _p(self.ctab), _p(self.stab),
+                                   _p(self.spec))
 
     def solve_rows(self, omega, pulse, ts, y0):
         N = self.N

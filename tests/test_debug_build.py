@@ -63,6 +63,6 @@ def test_debug_build_in_bounds_and_bit_exact(monkeypatch, name, n_osc, reward, m
         np.testing.assert_array_equal(obs.cpu().numpy(), ref["obs"])
         np.testing.assert_array_equal(rew.cpu().numpy(), ref["reward"])
     got, exp = sim.get_state(), o.state()
-    for key in ("y", "t", "ring", "wpos"):
+    for key in ("y", "t", "ring", "wpos", "spec"):
         np.testing.assert_array_equal(got[key], exp[key], err_msg=key)
     sim.close()

@@ -66,7 +66,7 @@ def test_step_max_steps_matches_oracle(torch_gpu):
     cfg.max_steps = 2
     sim, o = _pair(torch_gpu, cfg, alpha, omega, gs, gr, ct, st)
     sim.set_state(state)
-    o.y[:], o.t[:], o.step_count[:], o.ring[:], o.wpos[:] = (state[k] for k in ("y", "t", "step", "ring", "wpos"))
+    o.set_state(state)
     a = actions("rand", 7, cfg.n_elec, 0)
     with pytest.raises(abi.KuraSolverError, match="maximum number of solver steps"):
         sim.step(torch_gpu.from_numpy(a), check_errors=True)
@@ -76,7 +76,7 @@ def test_step_max_steps_matches_oracle(torch_gpu):
     for k in ("done", "reward", "nsamp"):
         np.testing.assert_array_equal(getattr(sim, k).cpu().numpy(), ref[k])
     g, r = sim.get_state(), o.state()
-    for k in ("y", "t", "step", "ring", "wpos"):
+    for k in ("y", "t", "step", "ring", "wpos", "spec"):
         np.testing.assert_array_equal(g[k], r[k], err_msg=k)
     np.testing.assert_array_equal(g["t"], state["t"])          # time and window not advanced
     sim.close()
@@ -89,7 +89,7 @@ def test_nonfinite_state_flags_only_that_env(torch_gpu):
     state["y"][4, 3] = np.inf
     sim, o = _pair(torch_gpu, cfg, alpha, omega, gs, gr, ct, st)
     sim.set_state(state)
-    o.y[:], o.t[:], o.step_count[:], o.ring[:], o.wpos[:] = (state[k] for k in ("y", "t", "step", "ring", "wpos"))
+    o.set_state(state)
     a = actions("rand", 6, cfg.n_elec, 3)
     sim.step(torch_gpu.from_numpy(a))
     ref = o.step(a)

@@ -102,7 +102,7 @@ def _run_pair(torch, name, N, B, reward, steps, act, check_every=1, gains=None, 
 
 
 def _cmp_state(g, o, where):
-    for k in ("y", "t", "step", "ring", "wpos"):
+    for k in ("y", "t", "step", "ring", "wpos", "spec"):
         if not np.array_equal(g[k], o[k]):
             bad = np.argwhere(g[k] != o[k])
             raise AssertionError(f"{where}: state[{k}] differs at {len(bad)} places, first {bad[:3].tolist()}: "
@@ -151,3 +151,41 @@ def test_phase_gate_1000_steps_env1_r2(torch_gpu):
     rel = np.abs(g["y"].astype(np.float64) - o["y"]) / np.maximum(np.abs(o["y"].astype(np.float64)), 1e-30)
     assert rel.max() <= PHASE_RTOL
     np.testing.assert_array_equal(g["y"], o["y"])
+
+
+def test_spectral_state_checkpoint(torch_gpu):
+    """R1's spectral accumulators through get_state/set_state: restored
+    exactly with 'spec' (kura_set_spec), re-formed from the ring without it
+    (kura_spec_init_kernel) bit-exactly as the oracle re-forms them."""
+    torch = torch_gpu
+    sim_mod = importlib.import_module("dbs-gym_amd.sim")
+    B = 19
+    cfg, alpha, omega, gs, gr, th0, ct, st, _ = make_case("env0", 256, B)
+    sim = sim_mod.KuraSim(cfg, 0)
+    sim.set_coupling(alpha)
+    sim.set_env_params(omega, gs, gr)
+    sim.set_spectral(ct, st)
+    o = ko.Oracle(cfg, alpha)
+    o.set_env_params(omega, gs, gr)
+    o.set_spectral(ct, st)
+    sim.reset(torch.from_numpy(th0))
+    o.reset(th0)
+    for k in range(5):
+        a = actions("rand", B, 1, k)
+        sim.step(torch.from_numpy(a))
+        o.step(a)
+    g = sim.get_state()
+    _cmp_state(g, o.state(), "after 5 steps")
+    sim.set_state({k: v for k, v in g.items() if k != "spec"})
+    o.set_state({k: v for k, v in o.state().items() if k != "spec"})
+    _cmp_state(sim.get_state(), o.state(), "re-formed")
+    sim.set_state(g)
+    np.testing.assert_array_equal(sim.get_state()["spec"], g["spec"])
+    o.set_state(g)
+    for k in range(3):
+        a = actions("rand", B, 1, 100 + k)
+        sim.step(torch.from_numpy(a))
+        ref = o.step(a)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(sim.reward.cpu().numpy(), ref["reward"])
+    sim.close()
