@@ -547,17 +547,16 @@ __device__ __forceinline__ void load8(const Slot& w, int slot, int t, float (&v)
 // carry their whole offset in the VGPR and soffset = 0, which puts them under
 // the recognizer's guard; the asm makes the lane offset opaque so the
 // per-(slot, tile) adds are not hoisted into long-lived registers.
-// KURA_SGPR_SOFFSET_STORES rebuilds the unguarded form (diagnosis only).
+// tools/check_store_hazards.py verifies the shipped machine code (a build
+// gate: __graft_entry__.build, tests/test_store_hazards.py); the unguarded
+// form is kept only as profiles/r04_sgpr_soffset_store.patch, which the test
+// builds to show that the checker flags it.
 __device__ __forceinline__ int opaque_vgpr(int v) {
     asm volatile("" : "+v"(v));
     return v;
 }
 __device__ __forceinline__ void store_rec_b128(const floatx4& v, __amdgpu_buffer_rsrc_t rs, int voff, int soff) {
-#ifdef KURA_SGPR_SOFFSET_STORES
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u32, v), rs, voff, soff, 0);
-#else
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u32, v), rs, opaque_vgpr(voff) + soff, 0, 0);
-#endif
 }
 __device__ __forceinline__ void store8(const Slot& w, int slot, int t, const float (&v)[8]) {
     // raw buffer stores through the same wave-uniform descriptor as the

@@ -1,0 +1,91 @@
+"""The store-data hazard as a build gate (DESIGN.md
+section 5): tools/check_store_hazards.py walks every control-flow path after
+each >8-byte VMEM store of the shipped machine code and flags a VALU write of
+the store's data VGPRs within 2 wait states.  CPU only (cross-compiled code)."""
+import importlib.util
+import os
+import shutil
+import subprocess
+
+import pytest
+
+from helpers import ROOT
+
+spec = importlib.util.spec_from_file_location("check_store_hazards", os.path.join(ROOT, "tools", "check_store_hazards.py"))
+chk = importlib.util.module_from_spec(spec)
+spec.loader.exec_module(chk)
+CSRC = os.path.join(ROOT, "dbs-gym_amd", "csrc")
+
+
+def _fn(lines):
+    """a synthetic llvm-objdump listing of one function"""
+    out = ["0000000000001000 <f>:"]
+    addr = 0x1000
+    for ln in lines:
+        insn, tgt = ln if isinstance(ln, tuple) else (ln, None)
+        out.append(f"\t{insn}  // {addr:012X}: 00000000" + (f" <f+0x{tgt:x}>" if tgt is not None else ""))
+        addr += 4
+    return "\n".join(out)
+
+
+def _branch(insn, target_off):
+    return (insn, target_off)
+
+
+def _hz(lines):
+    funcs = chk.parse(_fn(lines))
+    return chk.find_hazards(funcs)
+
+
+def test_detects_valu_write_right_after_wide_store():
+    assert _hz(["buffer_store_dwordx4 v[4:7], v0, s[8:11], s2 offen", "v_pk_add_f32 v[4:5], v[8:9], v[10:11]"])
+    assert _hz(["global_store_dwordx4 v[0:1], v[4:7], off", "s_mov_b32 s0, 1", "v_mov_b32_e32 v7, 0"])
+
+
+def test_wait_states_and_unrelated_registers_are_safe():
+    assert not _hz(["buffer_store_dwordx4 v[4:7], v0, s[8:11], 0 offen", "s_nop 1", "v_mov_b32_e32 v4, 0"])
+    assert not _hz(["buffer_store_dwordx4 v[4:7], v0, s[8:11], 0 offen", "s_mov_b32 s0, 1", "s_mov_b32 s1, 1",
+                    "v_mov_b32_e32 v4, 0"])
+    assert not _hz(["buffer_store_dwordx4 v[4:7], v0, s[8:11], 0 offen", "v_mov_b32_e32 v8, 0"])
+    assert not _hz(["buffer_store_dwordx2 v[4:5], v0, s[8:11], 0 offen", "v_mov_b32_e32 v4, 0"])   # 8 bytes
+    assert not _hz(["global_store_dwordx4 v[0:1], v[4:7], off", "v_mov_b32_e32 v0, 0"])   # address, not data
+
+
+def test_follows_branch_successors():
+    # store; s_cbranch to +0x10 (the v_mov writing v5): the taken path has 1 wait state
+    lines = ["buffer_store_dwordx4 v[4:7], v0, s[8:11], 0 offen", _branch("s_cbranch_execz 2", 0x10),
+             "s_nop 7", "s_nop 7", "v_mov_b32_e32 v5, 0"]
+    assert _hz(lines)
+    lines = ["buffer_store_dwordx4 v[4:7], v0, s[8:11], 0 offen", _branch("s_branch 2", 0x10),
+             "v_mov_b32_e32 v5, 0", "s_endpgm", "s_nop 0", "v_mov_b32_e32 v5, 0"]
+    assert not _hz(lines[:4] + ["s_nop 1", "v_mov_b32_e32 v5, 0"])   # taken path passes s_nop 1 first
+
+
+@pytest.mark.parametrize("name", ["libkura.so", "libkura_debug.so"])
+def test_shipped_libraries_are_hazard_free(name):
+    lib = os.path.join(CSRC, name)
+    if not os.path.exists(lib):
+        pytest.skip(f"{name} not built")
+    n, hz = chk.check_library(lib)
+    assert n > 100            # the records' wide stores are there
+    assert not hz, hz[:5]
+
+
+def test_old_sgpr_soffset_store_form_is_flagged(tmp_path):
+    """The round-2 record-store form (profiles/r04_sgpr_soffset_store.patch)
+    built from today's source: the gate must fail on it."""
+    if not os.path.exists("/opt/rocm/bin/hipcc"):
+        pytest.skip("no hipcc")
+    d = tmp_path / "src"
+    shutil.copytree(os.path.join(ROOT, "dbs-gym_amd", "csrc"), d / "dbs-gym_amd" / "csrc",
+                    ignore=shutil.ignore_patterns("*.so"))
+    shutil.copytree(os.path.join(ROOT, "include"), d / "include")
+    subprocess.run(["patch", "-p1", "-d", str(d), "-i", os.path.join(ROOT, "profiles", "r04_sgpr_soffset_store.patch")],
+                   check=True, capture_output=True)
+    import __graft_entry__ as ge
+    lib = str(tmp_path / "libkura_sgpr.so")
+    subprocess.run([ge.HIPCC, *ge.HIP_FLAGS, "-o", lib, str(d / "dbs-gym_amd" / "csrc" / "kura_kernels.hip")],
+                   check=True, capture_output=True)
+    _n, hz = chk.check_library(lib)
+    assert hz, "the checker did not flag the SGPR-soffset store form"
+    assert any(h[2] == "buffer_store_dwordx4" for h in hz)
