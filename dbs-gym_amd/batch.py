@@ -129,10 +129,15 @@ class EnvHost:
 
     def _conductances(self):
         """SimpleDBS conductances of the current contacts (env.py:106-156).  They
-        depend only on the contacts and the encapsulation modifier, which change
-        only at drift / spatial-variation events, so the last result is reused
-        until one of them changes (returned read-only)."""
-        key = (repr(self.elec_coords), repr(self.rec_coords), float(self.encapsulation_coeff))
+        depend only on the contacts, the encapsulation modifier and the
+        naive_dbs / directed_stimulation / grid_size settings (the reference
+        rebuilds SimpleDBS from params_dict at every reset, env.py:584-592),
+        which change only at drift / spatial-variation events or a set_attr,
+        so the last result is reused until one of them changes (returned
+        read-only)."""
+        p = self.p
+        key = (repr(self.elec_coords), repr(self.rec_coords), float(self.encapsulation_coeff),
+               repr(list(p["grid_size"])), bool(p["naive_dbs"]), bool(p.get("directed_stimulation")))
         if getattr(self, "_g_key", None) != key:
             p = self.p
             gs, naive = p["grid_size"], p["naive_dbs"]

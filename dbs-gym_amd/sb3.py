@@ -74,9 +74,26 @@ class KuraSB3VecEnv:
         obs, rew, term, trunc, info = self.venv.step(a)
         obs_h, rew64, term_h, trunc_h = self._to_host(obs, rew, term, trunc)
         dones = term_h | trunc_h
+        infos = [{} for _ in range(self.num_envs)]
+        # deferred failure checks: an env whose previous step failed was reset
+        # before this launch -- its episode ended (truncated) before this
+        # step's transition, which is the first of its new episode
+        pre = info.get("reset_before_step_ids", np.zeros(0, np.int64))
+        if len(pre):
+            pobs = info["reset_before_step_observation"].cpu().numpy()
+            now = time.time()
+            for j, b in enumerate(pre):
+                d = infos[b]
+                d["terminal_observation"] = pobs[j]
+                d["TimeLimit.truncated"] = True
+                if self.monitor:
+                    d["episode"] = {"r": round(float(self._ep_rew[b]), 6), "l": int(self._ep_len[b]),
+                                    "t": round(now - self._t0[b], 6)}
+                self._ep_rew[b] = 0.0
+                self._ep_len[b] = 0
+                self._t0[b] = now
         self._ep_rew += rew64
         self._ep_len += 1
-        infos = [{} for _ in range(self.num_envs)]
         ended = info.get("terminal_env_ids", np.zeros(0, np.int64))
         if len(ended):
             tobs = info["terminal_observation"].cpu().numpy()

@@ -71,10 +71,21 @@ class KuraVectorEnv:
     failure_check: "deferred" (default) -- the library's per-env failure
                 flags of a launch travel to the host by an asynchronous copy
                 into pinned memory and are acted on at the start of the next
-                step() (before its launch), so a step never blocks on the
-                device; a failed env reports done = 1 in the step it failed
-                (the kernel's own output) and is raised / reset one call later.
-                "eager": every step() synchronises and acts at once.
+                step() / reset() / close() (before its launch), so a step never
+                blocks on the device.  A failed env is reported one call late:
+                "raise" raises there; "reset" resets it before that call's
+                launch and reports the failed episode as truncated in that
+                call -- ``infos["reset_before_step_ids"]`` and
+                ``infos["reset_before_step_observation"]`` (its last
+                observation), ``failed_env_ids``/``failure_flags`` -- so an
+                SB3 wrapper closes the episode before counting that call's
+                transition (which belongs to the new episode).  In the failing
+                call itself the env is not reported done (terminated comes
+                from the episode counters, not the kernel's done = 1).
+                "eager": every step() synchronises and acts at once (the
+                failed env is truncated and autoreset in the same call).
+                Either way a solver failure ends the episode as truncated, not
+                terminated.
     """
 
     metadata = {"render.modes": ["human"]}
@@ -140,7 +151,8 @@ class KuraVectorEnv:
         # deferred failure flags: pinned host copies of the last step's and the
         # last autoreset's per-env flags, and the events that complete them
         self._pend = None          # (flags_pinned, event, reset_mask or None, reset_flags_pinned)
-        self._reset_fail_runs = np.zeros(B, np.int64)
+        self._reset_fail_runs = np.zeros(B, np.int64)   # consecutive failed resets per env
+        self._pending_gain = {}    # env -> float32(K/N) of a set_attr'd params_dict, applied at its next reset
         self._omega = np.zeros((B, self.N), np.float32)
         self._g_stim = np.zeros((B, self.n_elec, self.N))
         self._g_rec = np.zeros((B, max(self.cfg.n_rec, 1), self.N))
@@ -152,6 +164,10 @@ class KuraVectorEnv:
         parameters (one kura_set_env_params per contiguous run of envs)."""
         idx = sorted(int(b) for b in idx)
         t0 = time.perf_counter()
+        for b in idx:   # K of a set_attr'd params_dict: the reset builds KuramotoJAX with it (env.py:570-572)
+            if b in self._pending_gain:
+                self._gain[b] = self._pending_gain.pop(b)
+                self.sim.set_env_gain(self._gain[b:b + 1], env0=b)
         th = np.zeros((self.num_envs, self.N), np.float32)
         for b in idx:
             w0, gs, gr, th0 = self.hosts[b].reset_draws()
@@ -186,13 +202,20 @@ class KuraVectorEnv:
         if seed is not None:
             seeds = [seed + b for b in range(self.num_envs)] if np.isscalar(seed) else list(seed)
             self.np_random = [np.random.default_rng(int(x)) for x in seeds]
-        self._pend = None
+        infos: dict = {}
+        # deferred flags of the last step() (a failure there raises here in
+        # "raise" mode, as the reference's failing diffeqsolve would have)
+        pre_failed, pre_flags, pre_rfail = self._take_pending()
+        if self.on_failure == "raise" and (len(pre_failed) or len(pre_rfail)):
+            self._act_on_failures(pre_failed, pre_flags, pre_rfail, {}, "kura_step (previous call)")
+        if len(pre_failed):
+            infos["failed_env_ids"], infos["failure_flags"] = pre_failed, pre_flags
         th = self._draw(range(self.num_envs))
         obs = self.sim.reset(th)
-        self._check_reset(None)
+        self._check_reset(None, infos)
         self.steps[:] = 0
         self._was_reset = True
-        return obs.view(self.num_envs, 1, self.W).clone(), {}
+        return obs.view(self.num_envs, 1, self.W).clone(), infos
 
     def _failures_now(self):
         """Flags of the last launch, synchronously."""
@@ -213,6 +236,7 @@ class KuraVectorEnv:
         if rmask is not None:
             rf = np.where(rmask, rfl.numpy(), 0)
             ridx = np.nonzero(rf)[0]
+            self._reset_fail_runs[rmask & (rf == 0)] = 0      # those resets succeeded
         return idx, f[idx], ridx
 
     def _stash_flags(self, reset_mask=None):
@@ -250,8 +274,13 @@ class KuraVectorEnv:
         obs, rew, done = self.sim.step(a)
         self.steps += 1
         term_host = self.steps >= self.episode_steps
-        terminated = done.bool().clone()
+        # episode ends from the counters (== the kernel's done for every env whose
+        # step succeeded; the kernel also sets done = 1 for a failed env, which is
+        # reported as a truncation instead, below or one call later)
+        terminated = torch.from_numpy(term_host).to(self.device, non_blocking=True)
         truncated = torch.zeros_like(terminated)
+        if "reset_before_step_ids" in infos:
+            truncated[torch.as_tensor(infos["reset_before_step_ids"], device=self.device)] = True
         if self.failure_check == "eager":
             failed, fflags = self._failures_now()         # synchronises: the step's outputs are ready
             if len(failed):
@@ -306,6 +335,9 @@ class KuraVectorEnv:
             self.sim.raise_on_failure("kura_reset", None if mask is None else mask.to(self.device))
             return
         ridx, _ = self.sim.failed_envs(None if mask is None else mask.to(self.device))
+        ok = np.ones(self.num_envs, bool) if mask is None else mask.cpu().numpy().astype(bool)
+        ok[ridx] = False
+        self._reset_fail_runs[ok] = 0                    # a confirmed reset ends a run of failures
         if len(ridx):
             self._retry_resets(ridx, infos if infos is not None else {})
 
@@ -330,11 +362,14 @@ class KuraVectorEnv:
                 raise KuraSolverError(what, failed.tolist(), fflags.tolist())
             raise KuraSolverError("kura_reset (autoreset of the previous call)", rfailed.tolist(),
                                   [0] * len(rfailed))
-        ok = np.setdiff1d(np.arange(self.num_envs), rfailed)
-        self._reset_fail_runs[ok] = 0
         if len(failed):
             infos["failed_env_ids"] = failed
             infos["failure_flags"] = fflags
+            # the failed episodes end here (truncated): their last observation,
+            # before the reset below overwrites the buffer
+            infos["reset_before_step_ids"] = failed
+            infos["reset_before_step_observation"] = \
+                self.sim.obs[torch.as_tensor(failed, device=self.device)].clone().view(-1, 1, self.W)
         redo = np.union1d(failed, rfailed).astype(np.int64)
         if len(rfailed):
             self._reset_fail_runs[rfailed] += 1
@@ -426,11 +461,13 @@ class KuraVectorEnv:
 
     def set_attr(self, name: str, value, indices=None) -> None:
         """SB3 VecEnv.set_attr.  ``params_dict`` takes effect from the next
-        reset of those envs (the reference reads its params_dict there, and K
-        at every solve, env.py:264): per-reset draws, drift/spatial settings
-        and K follow the new dict; keys the batch's shared setup is built on
-        (N, grid, window, timing, reward, kernels) must stay equal or
-        ValueError is raised.  Other names raise AttributeError."""
+        reset of those envs, which is where the reference reads it: reset()
+        rebuilds KuramotoJAX(K=params_dict['K'], ...) (env.py:570-572) and
+        forward() then uses that fixed self.K (env.py:264).  Per-reset draws,
+        drift/spatial settings, conductances and K follow the new dict from
+        that reset on; keys the batch's shared setup is built on (N, grid,
+        window, timing, reward, kernels) must stay equal or ValueError is
+        raised.  Other names raise AttributeError."""
         idx = list(range(self.num_envs)) if indices is None else list(indices)
         if name != "params_dict":
             raise AttributeError(f"set_attr({name!r}) is not supported on the batched env")
@@ -449,9 +486,11 @@ class KuraVectorEnv:
                     newp[k] = old.get(k)
             self.params[i] = newp
             self.hosts[i].p = newp
-            if newp["K"] != old["K"]:
-                self._gain[i] = np.float32(newp["K"] / newp["num_oscillators"])
-                self.sim.set_env_gain(self._gain[i:i + 1], env0=i)
+            kn = np.float32(newp["K"] / newp["num_oscillators"])
+            if kn != self._gain[i]:
+                self._pending_gain[i] = kn          # applied by _draw at env i's next reset
+            else:
+                self._pending_gain.pop(i, None)
 
     def reward_of(self, windows, u0, kind: int = 0):
         """reward_* (env.py:638-688) of given 1-D windows (n, L) of any length L
@@ -489,7 +528,13 @@ class KuraVectorEnv:
         self._was_reset = True
 
     def close(self):
+        """Releases the handle; in "raise" mode a failure of the last step()
+        that was not yet read (deferred flags) is raised after the release."""
+        pre_failed, pre_flags, pre_rfail = self._take_pending() if self._pend is not None else ([], [], [])
         self.sim.close()
+        if self.on_failure == "raise" and (len(pre_failed) or len(pre_rfail)):
+            self._act_on_failures(np.asarray(pre_failed), np.asarray(pre_flags), np.asarray(pre_rfail), {},
+                                  "kura_step (last call before close)")
 
 
 class SpatialKuramoto:

@@ -207,9 +207,15 @@ def test_gpu_set_attr(gpu):
     p = copy.deepcopy(env.get_attr("params_dict")[0])
     p["K"] = 0.8
     p["init_state_mean"] = 1.0
+    g_before = env._gain.copy()
     env.set_attr("params_dict", p, [1])
     assert env.params[1]["K"] == 0.8 and env.hosts[1].p["init_state_mean"] == 1.0
-    assert env._gain[1] == np.float32(0.8 / p["num_oscillators"])
+    # K reaches the env at its next reset (KuramotoJAX is rebuilt there, env.py:570-572)
+    assert env._gain[1] == g_before[1] and env._pending_gain[1] == np.float32(0.8 / p["num_oscillators"])
+    env.step(np.zeros((env.num_envs, 1), np.float32))
+    assert env._gain[1] == g_before[1]
+    env.reset()
+    assert env._gain[1] == np.float32(0.8 / p["num_oscillators"]) and 1 not in env._pending_gain
     bad = copy.deepcopy(p)
     bad["observe_wind_counts"] = 10
     with pytest.raises(ValueError, match="observe_wind_counts"):
@@ -222,3 +228,31 @@ def test_gpu_set_attr(gpu):
         a.set_attr("reward_func", "x")
     assert a.obs_buffers is None      # DummyVecEnv fresh-copy observations by default
     a.close()
+
+
+@pytest.mark.gpu
+def test_gpu_set_attr_gain_applies_at_the_next_reset(gpu):
+    """a new K changes nothing until the env's next reset -- two
+    identical batches, one with a set_attr'd K, step identically until then,
+    and differ after it."""
+    torch = gpu
+    ea, eb = _venv(), _venv()
+    ea.reset()
+    eb.reset()
+    p = copy.deepcopy(ea.get_attr("params_dict")[0])
+    p["K"] = 0.8
+    ea.set_attr("params_dict", p, [0])
+    a = np.full((ea.num_envs, 1), 0.3, np.float32)
+    for _ in range(3):
+        _, ra, *_ = ea.step(a)
+        _, rb, *_ = eb.step(a)
+        assert torch.equal(ra, rb)
+    ea.reset()
+    eb.reset()
+    for _ in range(2):
+        _, ra, *_ = ea.step(a)
+        _, rb, *_ = eb.step(a)
+    ra, rb = ra.cpu().numpy(), rb.cpu().numpy()
+    assert ra[0] != rb[0] and np.array_equal(ra[1:], rb[1:])
+    ea.close()
+    eb.close()

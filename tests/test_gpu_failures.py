@@ -134,12 +134,15 @@ def test_vector_env_policies(torch_gpu, check):
     obs, rew, term, trunc, info = env.step(a)
     if check == "eager":
         assert list(info["failed_env_ids"]) == [1] and info["failure_flags"][0] == abi.KURA_F_NONFINITE
-        assert bool(trunc[1]) and bool(term[1]) and not bool(trunc[0])
+        assert bool(trunc[1]) and not bool(term[1]) and not bool(trunc[0])     # a truncation, not a termination
         assert list(info["terminal_env_ids"]) == [1] and env.steps[1] == 0 and env.steps[0] == 1
     else:
-        assert "failed_env_ids" not in info and bool(term[1]) and not bool(term[0])   # the kernel's done = 1
+        # not known yet: not done (episode counters), not truncated
+        assert "failed_env_ids" not in info and not bool(term[1]) and not bool(trunc[1])
         obs, rew, term, trunc, info = env.step(a)        # reported now; env 1 reset before this launch
         assert list(info["failed_env_ids"]) == [1] and info["failure_flags"][0] == abi.KURA_F_NONFINITE
+        assert list(info["reset_before_step_ids"]) == [1] and bool(trunc[1]) and not bool(term[1])
+        assert tuple(info["reset_before_step_observation"].shape) == (1, 1, env.W)
         assert env.steps[1] == 1 and env.steps[0] == 2 and np.isfinite(rew.cpu().numpy()).all()
     obs, rew, term, trunc, info = env.step(a)   # env 1 runs again after its reset
     assert "failed_env_ids" not in info and np.isfinite(rew.cpu().numpy()).all()
@@ -174,3 +177,97 @@ def test_vector_env_failed_resets_retry_then_raise(torch_gpu):
         env.reset()
     assert (env._reset_fail_runs == 3).all()
     env.close()
+
+
+def _nan_env(venv, p, n=3, **kw):
+    env = venv.KuraVectorEnv(p, num_envs=n, **kw)
+    env.reset()
+    st = env.sim.get_state()
+    st["y"][1, 0] = np.nan
+    env.sim.set_state(st)
+    return env
+
+
+def test_deferred_failure_raises_from_reset_and_close(torch_gpu):
+    """a failure of the last step before reset()/close() is not
+    dropped with the deferred flags: on_failure='raise' raises there."""
+    kura = importlib.import_module("dbs-gym_amd")
+    venv = importlib.import_module("dbs-gym_amd.vec_env")
+    p = kura.reference_params("env0", "eval", 0)
+    p["reward_func"] = "bbpow_action"
+    a = np.zeros((3, 1), np.float32)
+    env = _nan_env(venv, p)
+    env.step(a)
+    with pytest.raises(abi.KuraSolverError, match="previous call"):
+        env.reset()
+    env.close()
+    env = _nan_env(venv, p)
+    env.step(a)
+    with pytest.raises(abi.KuraSolverError, match="before close"):
+        env.close()
+    env = _nan_env(venv, p, on_failure="reset")
+    env.step(a)
+    obs, info = env.reset()                                   # reset mode: reported, every env reset
+    assert list(info["failed_env_ids"]) == [1]
+    env.step(a)
+    env.close()
+
+
+def test_deferred_failure_closes_the_sb3_episode(torch_gpu):
+    """with deferred checks an SB3 wrapper sees the failed episode
+    end (terminal_observation, TimeLimit.truncated, Monitor summary of the
+    steps before the failure) and the next one start."""
+    kura = importlib.import_module("dbs-gym_amd")
+    venv = importlib.import_module("dbs-gym_amd.vec_env")
+    sb3 = importlib.import_module("dbs-gym_amd.sb3")
+    p = kura.reference_params("env0", "eval", 0)
+    p["reward_func"] = "bbpow_action"
+    env = venv.KuraVectorEnv(p, num_envs=3, on_failure="reset")
+    v = sb3.KuraSB3VecEnv(env)
+    v.reset()
+    a = np.zeros((3, 1), np.float32)
+    v.step(a)
+    v.step(a)
+    st = env.sim.get_state()
+    st["y"][1, 0] = np.nan
+    env.sim.set_state(st)
+    obs, rew, dones, infos = v.step(a)                        # fails on the device; not known yet
+    assert not dones[1] and "terminal_observation" not in infos[1]
+    obs, rew, dones, infos = v.step(a)                        # closed here, before this transition
+    assert dones[1] and infos[1]["TimeLimit.truncated"] and infos[1]["terminal_observation"].shape == (1, env.W)
+    assert infos[1]["episode"]["l"] == 3 and infos[1]["failure_flags"] == abi.KURA_F_NONFINITE
+    assert not dones[0] and not dones[2]
+    assert v._ep_len[1] == 1 and v._ep_len[0] == 4 and np.isfinite(rew).all()
+    v.close()
+
+
+def test_reset_failure_runs_count_consecutive_failures_only(torch_gpu, monkeypatch):
+    """max_reset_failures counts failures in a row -- a confirmed
+    reset clears the count, so fail, succeed, fail, succeed does not raise."""
+    kura = importlib.import_module("dbs-gym_amd")
+    venv = importlib.import_module("dbs-gym_amd.vec_env")
+    p = kura.reference_params("env0", "eval", 0)
+    p["reward_func"] = "bbpow_action"
+    p["total_episode_len"] = 2 * (p["electrode_width"] + p["electrode_pause"])   # 2-step episodes
+    for check in ("eager", "deferred"):
+        env = venv.KuraVectorEnv(p, num_envs=2, on_failure="reset", max_reset_failures=1, failure_check=check)
+        host = env.hosts[0]
+        orig = host.reset_draws
+        calls = {"n": 0}
+        poison = {1, 3}          # reset draws 1 and 3 of env 0 get a NaN phase (its transient fails)
+
+        def draws():
+            w0, gs, gr, th = orig()
+            calls["n"] += 1
+            if calls["n"] - 1 in poison:
+                th = th.copy()
+                th[0] = np.nan
+            return w0, gs, gr, th
+        monkeypatch.setattr(host, "reset_draws", draws)
+        env.reset()                                            # draw 0: ok
+        a = np.zeros((2, 1), np.float32)
+        for _ in range(8):                                     # autoresets: draws 1 (fails), 2 (ok), 3 (fails), 4 ...
+            env.step(a)
+        assert calls["n"] >= 5
+        assert env._reset_fail_runs[0] == 0
+        env.close()

@@ -79,3 +79,25 @@ def test_synthetic_grids():
         assert coords.shape == (n, 3)
         assert ms.flat_index(p["elec_coords"][0], g) < n
         assert ms.flat_index(p["locus_center"], g) < n
+
+
+def test_conductance_cache_follows_the_stimulation_settings():
+    """naive_dbs / directed_stimulation changed through
+    params_dict (set_attr) rebuild the conductances at the next reset, as the
+    reference's SimpleDBS(params_dict) does (env.py:584-592)."""
+    import copy
+    import importlib
+    kura = importlib.import_module("dbs-gym_amd")
+    batch = importlib.import_module("dbs-gym_amd.batch")
+    p = kura.fill_driver_arrays(kura.reference_params("env0", "train"), w0_seed=3)
+    h = batch.EnvHost(p)
+    h.reset_draws()
+    gs0, _ = h._conductances()
+    q = copy.deepcopy(p)
+    q["directed_stimulation"] = True
+    h.p = q
+    gs1, _ = h._conductances()
+    assert not np.array_equal(gs0, gs1)
+    h2 = batch.EnvHost(q)
+    h2.reset_draws()
+    np.testing.assert_array_equal(gs1, h2._conductances()[0])
