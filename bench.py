@@ -82,7 +82,8 @@ def build_shard(args, rank):
         p["rand_seed"] = args.seed + gid
         if args.random_k:
             p["K"] = float(np.random.default_rng(args.seed * 7919 + gid).uniform(0.3, 0.8))
-        plist.append(kura.fill_driver_arrays(p, w0_seed=10_000_000 + args.seed + gid))
+        plist.append(p)
+    plist = kura.fill_driver_arrays_batch(plist, [10_000_000 + args.seed + rank * B + b for b in range(B)])
     hosts, shared = kura.build_batch(plist)
     omega, g_stim, g_rec, theta0 = kura.reset_arrays(hosts)
     cfg = sim_mod.make_config(base, B, reward_func=args.reward,

@@ -27,8 +27,9 @@ class EnvHost:
         p = params
         self.p = p
         if rs is None:
-            rs = np.random.RandomState()
-        rs.seed(p["rand_seed"])                                                # env.py:291
+            rs = np.random.RandomState(p["rand_seed"])                         # env.py:291
+        else:
+            rs.seed(p["rand_seed"])
         self.rs = rs
         self.reset_count = -1
         self.N = int(p["num_oscillators"])
@@ -81,6 +82,12 @@ class EnvHost:
     def reset_draws(self):
         """env.py:473-598 up to the transient: returns (w0 f64[N], g_stim f64[ne,N],
         g_rec f64[nr,N], theta0 f64[N])."""
+        w0, gs, gr, th = reset_draws_batch([self])
+        return w0[0], gs[0], gr[0], th[0]
+
+    def _advance_events(self):
+        """env.py:473-557: the reset counter and the drift / spatial-variation
+        events of this reset (their draws, in the reference's order)."""
         p = self.p
         self.reset_count += 1
         if p["temporal_drift"]:
@@ -117,14 +124,6 @@ class EnvHost:
                 self.rec_coords = [STIM_REC_LOCUS[index][1]]
                 self.spatial_var_episode += self.spatial_var_freq
                 self.spatial_events.append([self.reset_count, STIM_REC_LOCUS[index]])
-        w0 = ms.apply_locus_mask(self.w0_without_locus, p["locus_without_w0"], p["locus_mask"])  # env.py:566
-        w0 = ms.remove_negative_w0(self.rs, w0)                                # KuramotoJAX.__init__ env.py:213
-        if np.min(w0) < 0:
-            raise AssertionError("Natural frequencies w0 must be positive!")   # env.py:214
-        g_stim, g_rec = self._conductances()
-        theta0 = ms.initial_phases(self.rs, self.N, p["init_state_mean"], p["init_state_sd"])  # env.py:595-598
-        self.w0 = w0
-        return w0, g_stim, g_rec, theta0
 
 
     def _conductances(self):
@@ -139,16 +138,64 @@ class EnvHost:
         key = (repr(self.elec_coords), repr(self.rec_coords), float(self.encapsulation_coeff),
                repr(list(p["grid_size"])), bool(p["naive_dbs"]), bool(p.get("directed_stimulation")))
         if getattr(self, "_g_key", None) != key:
-            p = self.p
-            gs, naive = p["grid_size"], p["naive_dbs"]
-            g_stim = ms.conductances(self.grid, gs, self.elec_coords, self.encapsulation_coeff, naive)
-            g_rec = ms.conductances(self.grid, gs, self.rec_coords, self.encapsulation_coeff, naive)
-            if p.get("directed_stimulation"):                                  # env.py:125-140
-                g_stim = ms.directed_conductances(self.grid, gs, self.elec_coords, g_stim)
-            g_stim.setflags(write=False)
-            g_rec.setflags(write=False)
-            self._g_key, self._g = key, (g_stim, g_rec)
+            # shared by the envs of a process that sit on the same grid with the same contacts
+            ck = (self.grid.tobytes(),) + key
+            hit = _COND_CACHE.get(ck)
+            if hit is None:
+                gs, naive = p["grid_size"], p["naive_dbs"]
+                g_stim = ms.conductances(self.grid, gs, self.elec_coords, self.encapsulation_coeff, naive)
+                g_rec = ms.conductances(self.grid, gs, self.rec_coords, self.encapsulation_coeff, naive)
+                if p.get("directed_stimulation"):                              # env.py:125-140
+                    g_stim = ms.directed_conductances(self.grid, gs, self.elec_coords, g_stim)
+                g_stim.setflags(write=False)
+                g_rec.setflags(write=False)
+                hit = (g_stim, g_rec)
+                if len(_COND_CACHE) >= 256:
+                    _COND_CACHE.pop(next(iter(_COND_CACHE)))
+                _COND_CACHE[ck] = hit
+            self._g_key, self._g = key, hit
         return self._g
+
+
+_COND_CACHE: dict = {}   # (grid bytes, contacts, modifier, settings) -> read-only (g_stim, g_rec)
+
+
+def reset_draws_batch(hosts: list[EnvHost]):
+    """EnvHost.reset_draws of several envs, bit-identical to one call per env
+    (each env draws from its own stream, in the reference's order):
+      env.py:473-557  drift / spatial-variation events (per env);
+      env.py:566      w0 = apply_locus_mask(...)   (elementwise, all envs at once);
+      env.py:213      remove_negative_w0(w0): draws randn(k) only for the k <= 0
+                      entries -- none for a positive w0, so only envs with
+                      such entries take that call;
+      env.py:214      the positivity assertion;
+      env.py:595-598  theta0 = normal(mean, sd, N) per env, then
+                      remove_negative_w0(theta0) (again only when needed).
+    Returns (w0 (n, N), g_stim (n, ne, N), g_rec (n, nr, N), theta0 (n, N)),
+    float64; each host keeps its w0 (a row of the returned array)."""
+    for h in hosts:
+        h._advance_events()
+    w0wo = np.stack([h.w0_without_locus for h in hosts])
+    wl = np.stack([np.asarray(h.p["locus_without_w0"], np.float64) for h in hosts])
+    lm = np.stack([np.asarray(h.p["locus_mask"], np.float64) for h in hosts])
+    w0 = ms.apply_locus_mask(w0wo, wl, lm)                                      # env.py:566
+    neg = (w0 <= 0.).any(axis=1)
+    th = np.empty_like(w0)
+    gss, grs = [], []
+    for k, h in enumerate(hosts):
+        if neg[k]:
+            w0[k] = ms.remove_negative_w0(h.rs, w0[k])                          # env.py:213
+            if np.min(w0[k]) < 0:
+                raise AssertionError("Natural frequencies w0 must be positive!")   # env.py:214
+        g_stim, g_rec = h._conductances()
+        gss.append(g_stim)
+        grs.append(g_rec)
+        t = h.rs.normal(loc=h.p["init_state_mean"], scale=h.p["init_state_sd"], size=h.N)   # env.py:595-597
+        if (t <= 0.).any():
+            t = ms.remove_negative_w0(h.rs, t)                                  # env.py:598
+        th[k] = t
+        h.w0 = w0[k]
+    return w0, np.stack(gss), np.stack(grs), th
 
 
 def log_temporal_events(params: dict, host: EnvHost) -> str | None:
@@ -180,6 +227,51 @@ def fill_driver_arrays(params: dict, w0_seed: int | None = None, rs: np.random.R
     return p
 
 
+def fill_driver_arrays_batch(params_list: list[dict], w0_seeds) -> list[dict]:
+    """fill_driver_arrays for many envs at once, bit-identical to calling it
+    per env (tests/test_host.py): the grid, coordinates and locus mask are
+    built once per distinct geometry and shared (read-only) by every env's
+    dict; each env's two driver draws (rand(N) then uniform(N),
+    utils.py:868,927) come from its own MT19937 stream seeded w0_seeds[b];
+    the inverse-CDF transform and the locus blend run on the stacked (B, N)
+    draws.  The env dicts are shallow copies of the given ones plus the new
+    arrays.  (A per-env loop took ~1.1 s of bench.py's 1.64 s host setup at
+    4096 envs, BENCH_r03 extra.host_setup_s.)"""
+    B = len(params_list)
+    if B == 0:
+        return []
+    geo = {}
+    rs = np.random.RandomState()
+    N = int(params_list[0]["num_oscillators"])
+    rands = np.empty((B, N))
+    wls = np.empty((B, N))
+    keys = []
+    for b, p in enumerate(params_list):
+        if int(p["num_oscillators"]) != N:
+            raise ValueError("fill_driver_arrays_batch: every env must have the same num_oscillators")
+        key = (tuple(p["grid_size"]), float(p["coord_modif"]), tuple(p["locus_center"]), float(p["locus_size"]))
+        if key not in geo:
+            coords, grid = ms.neuron_grid_3d(*p["grid_size"], N, coord_modif=p["coord_modif"])
+            lm = ms.locus_mask(grid, p["grid_size"], p["locus_center"], p["locus_size"])
+            for a_ in (coords, grid, lm):
+                a_.setflags(write=False)
+            geo[key] = (coords, grid, lm)
+        keys.append(key)
+        rs.seed(w0_seeds[b])
+        rands[b] = rs.rand(N)                                                    # sample_w0 (utils.py:868)
+        wls[b] = rs.uniform(low=p["wmuL"] - p["wsdL"], high=p["wmuL"] + p["wsdL"], size=N)   # utils.py:927
+    w0_deg = ms.w0_from_uniform(rands)
+    out = []
+    for b, p in enumerate(params_list):
+        coords, grid, lm = geo[keys[b]]
+        w = ms.apply_locus_mask(w0_deg[b], wls[b], lm)
+        q = dict(p)
+        q.update(w0=w * 0.065, w0_without_locus=w0_deg[b] * 0.065, locus_without_w0=wls[b] * 0.065,
+                 locus_mask=lm, neur_coords=coords, neur_grid=grid)
+        out.append(q)
+    return out
+
+
 def build_batch(params_list: list[dict]) -> tuple[list[EnvHost], dict]:
     """Host setup for B envs sharing N, the grid and the spatial kernel: returns
     the EnvHost list and the shared coupling alpha (float64, env.py:219-229).
@@ -197,13 +289,8 @@ def build_batch(params_list: list[dict]) -> tuple[list[EnvHost], dict]:
 
 
 def reset_arrays(hosts: list[EnvHost], idx=None):
-    """Run reset_draws for the given envs and stack: omega f32, g_stim f64, g_rec f64, theta0 f32."""
+    """Run the reset draws of the given envs (reset_draws_batch) and stack:
+    omega f32, g_stim f64, g_rec f64, theta0 f32."""
     idx = range(len(hosts)) if idx is None else idx
-    ws, gss, grs, ths = [], [], [], []
-    for i in idx:
-        w, gs, gr, th = hosts[i].reset_draws()
-        ws.append(w)
-        gss.append(gs)
-        grs.append(gr)
-        ths.append(th)
-    return (np.stack(ws).astype(np.float32), np.stack(gss), np.stack(grs), np.stack(ths).astype(np.float32))
+    w, gs, gr, th = reset_draws_batch([hosts[i] for i in idx])
+    return w.astype(np.float32), gs, gr, th.astype(np.float32)

@@ -117,12 +117,18 @@ def _w0_inverse_cdf(lf_peak=6, beta_peak=10):
 _INV_CDF = None
 
 
-def sample_w0(rs: np.random.RandomState, n: int) -> np.ndarray:
-    """utils.py:847-882 generate_w0_samples: inverse-CDF samples (Hz-like)."""
+def w0_from_uniform(u: np.ndarray) -> np.ndarray:
+    """The inverse-CDF transform of generate_w0_samples (utils.py:868-882) on
+    uniform draws of any shape (elementwise)."""
     global _INV_CDF
     if _INV_CDF is None:
         _INV_CDF = _w0_inverse_cdf()
-    return _INV_CDF(rs.rand(n))
+    return _INV_CDF(u)
+
+
+def sample_w0(rs: np.random.RandomState, n: int) -> np.ndarray:
+    """utils.py:847-882 generate_w0_samples: inverse-CDF samples (Hz-like)."""
+    return w0_from_uniform(rs.rand(n))
 
 
 def locus_mask(neur_grid, grid_size, locus_coord, locus_size) -> np.ndarray:

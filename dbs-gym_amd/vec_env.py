@@ -23,7 +23,7 @@ import torch
 
 from . import spectral
 from .abi import KURA_S_MAX
-from .batch import EnvHost, build_batch, fill_driver_arrays, log_temporal_events
+from .batch import EnvHost, build_batch, fill_driver_arrays, fill_driver_arrays_batch, log_temporal_events, reset_draws_batch
 from .abi import KuraSolverError
 from .sim import KuraSim, make_config
 
@@ -116,11 +116,13 @@ class KuraVectorEnv:
         if rand_seeds is not None:
             for p, s in zip(plist, rand_seeds):
                 p["rand_seed"] = int(s)
-        for b, p in enumerate(plist):
-            if p.get("w0") is None or p.get("neur_grid") is None:
-                plist[b] = fill_driver_arrays(p, w0_seed=w0_seed + b)
-            if reward_func is not None:
-                plist[b]["reward_func"] = reward_func
+        todo = [b for b, p in enumerate(plist) if p.get("w0") is None or p.get("neur_grid") is None]
+        if todo:   # train_aDBS_RL.py:95-112, from RandomState(w0_seed + b) per env
+            for b, q in zip(todo, fill_driver_arrays_batch([plist[b] for b in todo], [w0_seed + b for b in todo])):
+                plist[b] = q
+        if reward_func is not None:
+            for p in plist:
+                p["reward_func"] = reward_func
         self.params = plist
         self.num_envs = B = num_envs
         self.hosts, shared = build_batch(plist)
@@ -169,13 +171,14 @@ class KuraVectorEnv:
                 self._gain[b] = self._pending_gain.pop(b)
                 self.sim.set_env_gain(self._gain[b:b + 1], env0=b)
         th = np.zeros((self.num_envs, self.N), np.float32)
-        for b in idx:
-            w0, gs, gr, th0 = self.hosts[b].reset_draws()
-            self._log_events(b)
-            self._omega[b] = w0.astype(np.float32)
-            self._g_stim[b] = gs
-            self._g_rec[b] = gr
-            th[b] = th0.astype(np.float32)
+        if idx:
+            w0, gs, gr, th0 = reset_draws_batch([self.hosts[b] for b in idx])
+            for b in idx:
+                self._log_events(b)
+            self._omega[idx] = w0.astype(np.float32)
+            self._g_stim[idx] = gs
+            self._g_rec[idx] = gr
+            th[idx] = th0.astype(np.float32)
         self._t_draw = time.perf_counter() - t0
         k = 0
         while k < len(idx):

@@ -101,3 +101,35 @@ def test_conductance_cache_follows_the_stimulation_settings():
     h2 = batch.EnvHost(q)
     h2.reset_draws()
     np.testing.assert_array_equal(gs1, h2._conductances()[0])
+
+
+def test_batched_driver_fill_and_reset_draws_are_bit_identical():
+    """fill_driver_arrays_batch / reset_draws_batch (the vectorised host setup
+    of bench.py and KuraVectorEnv) give exactly the per-env functions' arrays
+    and leave every env's RNG stream in the same state."""
+    import copy
+    import importlib
+    kura = importlib.import_module("dbs-gym_amd")
+    batch = importlib.import_module("dbs-gym_amd.batch")
+    base = kura.reference_params("env2", "train")
+    plist = []
+    for b in range(12):
+        p = dict(base)
+        p["rand_seed"] = 40 + b
+        plist.append(p)
+    seeds = [900 + b for b in range(12)]
+    one = [kura.fill_driver_arrays(p, w0_seed=s) for p, s in zip(plist, seeds)]
+    many = batch.fill_driver_arrays_batch(plist, seeds)
+    for a, b in zip(one, many):
+        for k in ("w0", "w0_without_locus", "locus_without_w0", "locus_mask", "neur_coords", "neur_grid"):
+            np.testing.assert_array_equal(np.asarray(a[k]), np.asarray(b[k]), err_msg=k)
+    h1 = [batch.EnvHost(copy.deepcopy(p)) for p in one]
+    h2 = [batch.EnvHost(copy.deepcopy(p)) for p in one]
+    for _ in range(5):    # env2: drift events at some of these resets
+        r1 = [h.reset_draws() for h in h1]
+        r2 = batch.reset_draws_batch(h2)
+        for k in range(4):
+            np.testing.assert_array_equal(np.stack([r[k] for r in r1]), r2[k])
+    for a, b in zip(h1, h2):
+        sa, sb = a.rs.get_state(), b.rs.get_state()
+        assert np.array_equal(sa[1], sb[1]) and sa[2:] == sb[2:]
