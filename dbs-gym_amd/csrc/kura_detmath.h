@@ -119,6 +119,65 @@ KDM_FN void kdm_sincosf(float x, float* s_out, float* c_out) {
 }
 
 
+// sin and cos of fmod(y, 2pi_f) -- env.py:253-255's theta = jnp.fmod(y, 2*pi)
+// followed by the sin of phase differences (factorised into sin/cos of theta)
+// -- with the 2pi_f reduction folded into the Cody-Waite reduction.
+// 2pi_f = (float)(2 pi) = 4 * C1 exactly.  With k = trunc(y / 2pi_f) (fmod's
+// quotient, estimated as trunc(y * (1/2pi)_f) without fmod's exact
+// correction steps), n = rint(y * 2/pi_f) and j = n - 4k:
+//     r = y - n*C1 - j*C2 - j*C3 = (y - k*2pi_f) - j*(C1 + C2 + C3),
+// the Cody-Waite remainder of theta_k = y - k*2pi_f with quadrant j & 3.
+// That is fmod(y, 2pi_f)'s remainder whenever the estimated k is fmod's
+// quotient; it is off by one only for y within a few ulp(y) of a multiple of
+// 2pi_f (theta within ~1e-3 rad of 0 or 2pi_f at |y| ~ 5e3), where the sine's
+// argument then moves by 2pi - 2pi_f = 1.7e-7 rad -- inside the RHS pin
+// against the reference's op sequence (tests/test_golden_reference.py).
+// fmaf(-n, C1, y) is exact-then-rounded-once, like fmaf(-j, C1, fmod(y)) in
+// the unfolded form, so away from those points the result is the unfolded
+// one's accuracy; the separate fmod pass and its corrections are gone (the
+// stage input's VALU work per element drops by about a sixth).  Valid for
+// |y| < 2^22; the piecewise definition below takes the exact fmod +
+// kdm_sincosf path beyond (never reached in practice: ~4e6 rad).
+KDM_FN void kdm_sincos_red(float r, int q, float* s_out, float* c_out) {
+    float z = r * r;
+    float ps = KDM_FMAF(z, -1.9515295891e-4f, 8.3321608736e-3f);
+    ps = KDM_FMAF(z, ps, -1.6666654611e-1f);
+    float sr = KDM_FMAF(r * z, ps, r);
+    float pc = KDM_FMAF(z, 2.443315711809948e-5f, -1.388731625493765e-3f);
+    pc = KDM_FMAF(z, pc, 4.166664568298827e-2f);
+    float cr = KDM_FMAF(z * z, pc, KDM_FMAF(-0.5f, z, 1.0f));
+    float s = (q & 1) ? cr : sr;
+    float c = (q & 1) ? sr : cr;
+    s = (q & 2) ? -s : s;
+    c = ((q + 1) & 2) ? -c : c;
+    *s_out = s;
+    *c_out = c;
+}
+
+// fast path (|y| < 2^22; sets *slow otherwise): reduced argument and quadrant
+KDM_FN float kdm_fold_reduce(float y, int* q, int* slow) {
+    const float k = truncf(y * KDM_INV_TWO_PI_F);
+    const float n = rintf(y * KDM_TWO_OVER_PI_F);
+    const int j = (int)n - 4 * (int)k;
+    const float jf = (float)j;
+    float r = KDM_FMAF(-n, KDM_PIO2_C1, y);
+    r = KDM_FMAF(-jf, KDM_PIO2_C2, r);
+    r = KDM_FMAF(-jf, KDM_PIO2_C3, r);
+    *q = j & 3;
+    *slow |= !(fabsf(y) < 4194304.0f);
+    return r;
+}
+
+KDM_FN void kdm_sincos_fmod2pi(float y, float* s_out, float* c_out) {
+    int slow = 0, q;
+    const float r = kdm_fold_reduce(y, &q, &slow);
+    if (!slow) {
+        kdm_sincos_red(r, q, s_out, c_out);
+        return;
+    }
+    kdm_sincosf(kdm_fmod2pi(y), s_out, c_out);  // |y| >= 2^22, inf, nan
+}
+
 KDM_FN float kdm_cosf(float x) {
     float s, c;
     kdm_sincosf(x, &s, &c);

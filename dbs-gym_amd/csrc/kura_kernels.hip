@@ -660,7 +660,7 @@ __device__ __forceinline__ void stage_input(const Slot& ws, float* Xs, int s STA
         if (t + 1 < TPW) fetch(t + 1, b ^ 1);
 #endif
         const int i = 32 * (wave * TPW + t) + (lane & 31);
-        float ys[8], th[8];
+        float ys[8];
         int slow = 0;
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
@@ -677,16 +677,17 @@ __device__ __forceinline__ void stage_input(const Slot& ws, float* Xs, int s STA
                 v = y0[b][q] + acc;
             }
             ys[q] = v;
-            th[q] = kdm_fmod2pi_fast(v, &slow);
         }
-        if (__builtin_expect(__any(slow), 0)) {  // |y| >= 2^22: never in practice
-#pragma unroll
-            for (int q = 0; q < 8; ++q) th[q] = kdm_fmod2pi(ys[q]);
-        }
+        // theta = fmod(ys, 2pi_f) folded into the sincos reduction
+        // (kdm_sincos_fmod2pi, kura_detmath.h): branch-free for the tile
 #ifdef KURA_STAMPS_SI
         float snv[8], csv[8];
 #pragma unroll
-        for (int q = 0; q < 8; ++q) kdm_sincosf(th[q], &snv[q], &csv[q]);
+        for (int q = 0; q < 8; ++q) {
+            int qd;
+            const float r = kdm_fold_reduce(ys[q], &qd, &slow);
+            kdm_sincos_red(r, qd, &snv[q], &csv[q]);
+        }
         asm volatile("" ::: "memory");
         STAMP(17);
 #pragma unroll
@@ -695,20 +696,31 @@ __device__ __forceinline__ void stage_input(const Slot& ws, float* Xs, int s STA
             Xs[xs_idx(e, i)] = snv[q];
             Xs[xs_idx(16 + e, i)] = csv[q];
         }
-        if (s == 6) store8(ws, SL_Y1, t, ys);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         STAMP(18);
 #else
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
             float sn, cs;
-            kdm_sincosf(th[q], &sn, &cs);
+            int qd;
+            const float r = kdm_fold_reduce(ys[q], &qd, &slow);
+            kdm_sincos_red(r, qd, &sn, &cs);
             const int e = mfma_env(q, lane);
             Xs[xs_idx(e, i)] = sn;
             Xs[xs_idx(16 + e, i)] = cs;
         }
-        if (s == 6) store8(ws, SL_Y1, t, ys);
 #endif
+        if (__builtin_expect(__any(slow), 0)) {  // some |y| >= 2^22 (never in practice): exact fmod path
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                float sn, cs;
+                kdm_sincos_fmod2pi(ys[q], &sn, &cs);
+                const int e = mfma_env(q, lane);
+                Xs[xs_idx(e, i)] = sn;
+                Xs[xs_idx(16 + e, i)] = cs;
+            }
+        }
+        if (s == 6) store8(ws, SL_Y1, t, ys);
     }
 }
 
@@ -2039,19 +2051,24 @@ __global__ __launch_bounds__(64) void kura_reward_n_kernel(DevParams p, const do
 #include "kura_fft.inc"
 
 // ------------------------------------------------------------- self-tests --
+#define KURA_SELFTEST_MATH_W 10
 __global__ void kura_selftest_math_kernel(const float* x, const float* y, float* out, int n) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
+    float* o = out + (size_t)i * KURA_SELFTEST_MATH_W;
     float s, c;
     kdm_sincosf(x[i], &s, &c);
-    out[(size_t)i * 8 + 0] = s;
-    out[(size_t)i * 8 + 1] = c;
-    out[(size_t)i * 8 + 2] = kdm_fmod2pi(x[i]);
-    out[(size_t)i * 8 + 3] = kdm_inv_fifth_root(fabsf(y[i]));
-    out[(size_t)i * 8 + 4] = sqrtf(fabsf(x[i]));
-    out[(size_t)i * 8 + 5] = x[i] / y[i];
-    out[(size_t)i * 8 + 6] = (float)((double)x[i] / (double)y[i]);
-    out[(size_t)i * 8 + 7] = (float)ceil((double)x[i] / 0.05);
+    o[0] = s;
+    o[1] = c;
+    o[2] = kdm_fmod2pi(x[i]);
+    o[3] = kdm_inv_fifth_root(fabsf(y[i]));
+    o[4] = sqrtf(fabsf(x[i]));
+    o[5] = x[i] / y[i];
+    o[6] = (float)((double)x[i] / (double)y[i]);
+    o[7] = (float)ceil((double)x[i] / 0.05);
+    kdm_sincos_fmod2pi(x[i], &s, &c);   // the RHS's theta = fmod(y, 2pi_f) -> sin, cos
+    o[8] = s;
+    o[9] = c;
 }
 
 // One 32-row coupling GEMM through the production GEMM path.

@@ -251,9 +251,9 @@ int kura_get_env_flags(KuraHandle* h, int32_t* out_dev, void* stream);
 int kura_get_stats(KuraHandle* h, int64_t* out, int n);
 
 /* diagnostics for the GPU parity tests (host pointers; synchronous; not on
- * the step path).  selftest_math writes 8 floats per element: sin, cos,
+ * the step path).  selftest_math writes 10 floats per element: sin, cos,
  * fmod2pi, inv_fifth_root(|y|), sqrt(|x|), x/y, f32(f64 x / f64 y),
- * ceil(x/0.05).  selftest_gemm runs the production MFMA coupling GEMM on one
+ * ceil(x/0.05), and sin, cos of fmod(x, 2pi_f) (the RHS's folded reduction).  selftest_gemm runs the production MFMA coupling GEMM on one
  * 32 x N operand: Y[r][i] = sum_k X[r][k] * alpha[i][k]. */
 int kura_selftest_math(const float* x, const float* y, float* out, int n);
 int kura_selftest_gemm(const float* X, const float* alpha, float* Y, int N);

@@ -295,17 +295,16 @@ static void work_free(Work* w) {
 
 /* -------------------------------------------------------------------- RHS
  * env.py:252-256:  theta = fmod(y, 2pi);  dy_i = w_i + (K/N) sum_j a_ij
- * sin(theta_j - theta_i) + pulse_i.  Restated with the exact identity
+ * sin(theta_j - theta_i) + pulse_i.  s_j, c_j = sin, cos of fmod(y_j, 2pi_f)
+ * with the fmod folded into the Cody-Waite reduction (kdm_sincos_fmod2pi,
+ * kura_detmath.h).  Restated with the exact identity
  * sin(tj - ti) = s_j c_i - c_j s_i:
  *   P_i = sum_j a_ij s_j,  Q_i = sum_j a_ij c_j   (fmaf chain, j ascending, from +0)
  *   coup_i = fmaf(c_i, P_i, -(s_i*Q_i));  f_i = fmaf(kn, coup_i, w_i) + pulse_i
  */
 static void rhs(const OCtx* o, Work* w, const float* y, const float* omega, const float* pulse, float* f) {
     const int N = o->N;
-    for (int j = 0; j < N; ++j) {
-        float th = kdm_fmod2pi(y[j]);
-        kdm_sincosf(th, &w->s[j], &w->c[j]);
-    }
+    for (int j = 0; j < N; ++j) kdm_sincos_fmod2pi(y[j], &w->s[j], &w->c[j]);   /* theta = fmod(y, 2pi_f) */
     enum { IB = 256 };
     for (int ib = 0; ib < N; ib += IB) {
         int ie = ib + IB < N ? ib + IB : N;
@@ -815,6 +814,9 @@ void oracle_rhs(void* ctx, const float* y, const float* omega, const float* puls
 
 void oracle_sincos(const float* x, float* s, float* c, int n) {
     for (int i = 0; i < n; ++i) kdm_sincosf(x[i], &s[i], &c[i]);
+}
+void oracle_sincos_fmod2pi(const float* x, float* s, float* c, int n) {
+    for (int i = 0; i < n; ++i) kdm_sincos_fmod2pi(x[i], &s[i], &c[i]);
 }
 void oracle_fmod2pi(const float* x, float* r, int n) {
     for (int i = 0; i < n; ++i) r[i] = kdm_fmod2pi(x[i]);

@@ -54,7 +54,7 @@ def lib() -> ctypes.CDLL:
         L.oracle_r64_f64.argtypes = [c_void_p, c_int]
         L.oracle_arange.restype = c_int
         L.oracle_arange.argtypes = [c_double, c_double, c_double, c_void_p, c_int]
-        for n in ("oracle_sincos",):
+        for n in ("oracle_sincos", "oracle_sincos_fmod2pi"):
             getattr(L, n).argtypes = [c_void_p, c_void_p, c_void_p, c_int]
         for n in ("oracle_fmod2pi", "oracle_inv_fifth_root"):
             getattr(L, n).argtypes = [c_void_p, c_void_p, c_int]
@@ -193,6 +193,15 @@ def sincos(x):
     s = np.empty_like(x)
     c = np.empty_like(x)
     lib().oracle_sincos(_p(x), _p(s), _p(c), x.size)
+    return s, c
+
+
+def sincos_fmod2pi(x):
+    """sin, cos of fmod(x, 2pi_f) as the RHS takes them (kdm_sincos_fmod2pi)"""
+    x = np.ascontiguousarray(x, np.float32)
+    s = np.empty_like(x)
+    c = np.empty_like(x)
+    lib().oracle_sincos_fmod2pi(_p(x), _p(s), _p(c), x.size)
     return s, c
 
 

@@ -67,3 +67,31 @@ def test_r64_order():
         assert ko.r64_f32(x) == p[0]
         xd = x.astype(np.float64)
         assert abs(ko.r64_f64(xd) - xd.sum()) <= 1e-12 * max(1, np.abs(xd).sum())
+
+
+def test_folded_fmod_sincos_matches_sin_of_fmod():
+    """kdm_sincos_fmod2pi (the RHS: sin/cos of theta = fmod(y, 2pi_f) with the
+    fmod folded into the Cody-Waite reduction) against libm's sin/cos of the
+    exact float32 fmod in float64: within the unfolded form's accuracy, plus
+    2pi - 2pi_f = 1.7e-7 rad where the folded quotient differs from fmod's
+    (|y| near a multiple of 2pi_f)."""
+    rng = np.random.default_rng(4)
+    two_pi_f = np.float32(2 * np.pi)
+    x = np.concatenate([rng.uniform(0, 2 * np.pi, 200_000), rng.uniform(0, 6000, 400_000),
+                        rng.uniform(-50, 50, 100_000), np.arange(-40, 40) * np.float64(two_pi_f),
+                        np.arange(1, 4000) * np.float64(two_pi_f) + 1e-4]).astype(np.float32)
+    s, c = ko.sincos_fmod2pi(x)
+    th = np.fmod(x, two_pi_f).astype(np.float64)     # the reference's theta (exact)
+    for got, ref in ((s, np.sin(th)), (c, np.cos(th))):
+        assert np.abs(got - ref).max() <= 4e-7
+    # away from the 2pi_f boundaries it is the unfolded result's accuracy (<= 3 ulp)
+    far = (np.abs(th) > 2e-3) & (np.abs(np.abs(th) - float(two_pi_f)) > 2e-3)
+    for got, ref in ((s, np.sin(th)), (c, np.cos(th))):
+        big = far & (np.abs(ref) > 1e-3)
+        assert _ulp_err(got[big], ref[big]).max() <= 3.0
+    # beyond 2^22 the exact fmod path is taken
+    xs = np.array([5e6, -3e7, 2.0 ** 23 + 1], np.float32)
+    s2, c2 = ko.sincos_fmod2pi(xs)
+    s3, c3 = ko.sincos(ko.fmod2pi(xs))
+    np.testing.assert_array_equal(s2, s3)
+    np.testing.assert_array_equal(c2, c3)

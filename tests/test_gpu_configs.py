@@ -186,3 +186,59 @@ def test_env2_b4096_vector_env_sampled(torch_gpu):
             np.testing.assert_array_equal(obs[idx, 0].cpu().numpy(), ref["obs"])
     np.testing.assert_array_equal(env.sim.get_state()["y"][idx], o.state()["y"])
     env.close()
+
+
+def test_env2_phase_gate_1000_steps_vector_env(torch_gpu):
+    """The north_star gate on env2: drift events and
+    per-env K ~ U(0.3, 0.8) at N=1024 through KuraVectorEnv, 1000 steps with
+    300-step episodes (3 autoresets per env, each with the reference's drift
+    draws), rewards every step and phases at the end bit-exact against the
+    oracle (hence within 1e-5 relative), the reset draws replayed by fresh
+    EnvHosts."""
+    vec = importlib.import_module("dbs-gym_amd.vec_env")
+    import copy
+    B, N, L = 8, 1024, 300
+    base = kura.fill_driver_arrays(kura.synthetic_params("env2", N), w0_seed=77)
+    Ks = np.random.default_rng(19).uniform(0.3, 0.8, B)
+    plist = []
+    for b in range(B):
+        p = copy.copy(base)
+        p["K"] = float(Ks[b])
+        p["rand_seed"] = 500 + b
+        plist.append(p)
+    env = vec.KuraVectorEnv(plist, reward_func="bbpow_action")
+    env.episode_steps = L
+    c = copy.copy(env.cfg)
+    o = ko.Oracle(c, env._alpha.astype(np.float32))
+    o.set_gain(np.array([np.float32(p["K"] / N) for p in plist], np.float32))
+    bins = kura.spectral.beta_bins(c.window, base["verbose_dt"])
+    o.set_spectral(*kura.spectral.twiddles(c.window, bins))
+    hosts = [kura.EnvHost(copy.deepcopy(p)) for p in plist]
+
+    def draw():
+        w0, gs, gr, th = kura.reset_draws_batch(hosts)
+        o.set_env_params(w0.astype(np.float32), gs, gr)
+        return th.astype(np.float32)
+
+    obs, _ = env.reset()
+    np.testing.assert_array_equal(obs[:, 0].cpu().numpy(), o.reset(draw()))
+    rng = np.random.default_rng(5)
+    resets = 0
+    for k in range(1000):
+        a = rng.uniform(-1, 1, (B, c.n_elec)).astype(np.float32)
+        obs, rew, term, trunc, info = env.step(a)
+        ref = o.step(a)
+        np.testing.assert_array_equal(rew.cpu().numpy(), ref["reward"], err_msg=f"reward step {k}")
+        if (k + 1) % L == 0:
+            resets += 1
+            assert len(info["terminal_env_ids"]) == B
+            np.testing.assert_array_equal(info["terminal_observation"][:, 0].cpu().numpy(), ref["obs"])
+            np.testing.assert_array_equal(obs[:, 0].cpu().numpy(), o.reset(draw()))
+            np.testing.assert_array_equal(env.sim.get_state()["y"], o.state()["y"])   # after the reset
+    assert resets == 3
+    g, r = env.sim.get_state(), o.state()
+    for key in ("y", "t", "step", "ring", "wpos", "spec"):
+        np.testing.assert_array_equal(g[key], r[key], err_msg=key)
+    rel = np.abs(g["y"].astype(np.float64) - r["y"]) / np.maximum(np.abs(r["y"].astype(np.float64)), 1e-30)
+    assert rel.max() <= 1e-5
+    env.close()

@@ -43,7 +43,7 @@ def test_detmath_bitwise(lib):
                         rng.uniform(-1e4, 1e4, n // 4), rng.normal(0, 1, n // 4)]).astype(np.float32)
     y = np.concatenate([rng.uniform(1e-6, 10, n // 2), rng.uniform(-5, 5, n // 2)]).astype(np.float32)
     y[y == 0] = 1.0
-    out = np.zeros((n, 8), np.float32)
+    out = np.zeros((n, 10), np.float32)
     assert lib.kura_selftest_math(x.ctypes.data, y.ctypes.data, out.ctypes.data, n) == 0
     s, c = ko.sincos(x)
     np.testing.assert_array_equal(out[:, 0], s)
@@ -54,6 +54,9 @@ def test_detmath_bitwise(lib):
     np.testing.assert_array_equal(out[:, 5], x / y)
     np.testing.assert_array_equal(out[:, 6], (x.astype(np.float64) / y.astype(np.float64)).astype(np.float32))
     np.testing.assert_array_equal(out[:, 7], np.ceil(x.astype(np.float64) / 0.05).astype(np.float32))
+    sf, cf = ko.sincos_fmod2pi(x)
+    np.testing.assert_array_equal(out[:, 8], sf)
+    np.testing.assert_array_equal(out[:, 9], cf)
 
 
 @pytest.mark.parametrize("N", [256, 512, 1024])
