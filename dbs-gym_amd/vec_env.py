@@ -158,6 +158,7 @@ class KuraVectorEnv:
         self._omega = np.zeros((B, self.N), np.float32)
         self._g_stim = np.zeros((B, self.n_elec, self.N))
         self._g_rec = np.zeros((B, max(self.cfg.n_rec, 1), self.N))
+        self._theta0 = np.zeros((B, self.N))      # init_state of each env's last reset (env.py:594-598)
         self._was_reset = False
 
     # ---- gymnasium VectorEnv API --------------------------------------------
@@ -178,6 +179,7 @@ class KuraVectorEnv:
             self._omega[idx] = w0.astype(np.float32)
             self._g_stim[idx] = gs
             self._g_rec[idx] = gr
+            self._theta0[idx] = th0
             th[idx] = th0.astype(np.float32)
         self._t_draw = time.perf_counter() - t0
         k = 0
@@ -454,6 +456,10 @@ class KuraVectorEnv:
             return [getattr(self.hosts[i], name) for i in idx]
         if name == "np_random":
             return [self.np_random[i] for i in idx]
+        if name == "init_state":                                    # env.py:594-598 (float64 draws)
+            return [self._theta0[i].copy() for i in idx]
+        if name in _UNSERVED:
+            raise AttributeError(_UNSERVED[name])
         raise AttributeError(name)
 
     # params the batch is built around: they cannot change on a running handle
@@ -540,6 +546,16 @@ class KuraVectorEnv:
                                   "kura_step (last call before close)")
 
 
+# reference attributes the GPU path does not keep (no caller in the reference
+# reads them: aDBS_RL/, the notebooks); asking for them raises with the reason
+_UNSERVED = {
+    "theta_record_transient": "theta_record_transient (env.py:611: the LFP of all 3999 transient rows) is not kept: "
+                              "the reset kernel forms only the last W samples, the observation window "
+                              "(theta_state / the reset's obs); the first 3999 - W rows feed no output and are "
+                              "not evaluated (DESIGN.md section 5, K2)",
+}
+
+
 class SpatialKuramoto:
     """Single-env drop-in for environment/env.py:274 SpatialKuramoto."""
 
@@ -563,12 +579,16 @@ class SpatialKuramoto:
         """env.py:467-614.  ``seed`` seeds gymnasium's np_random only
         (env.py:471): the draws continue the env's global-RNG stream."""
         obs, info = self._v.reset(seed=None if seed is None else [int(seed)])
+        self._n_on = None
         self.current_step = 0
         self.done = False
         self.theta_state = obs[0].cpu().numpy()
         return self.theta_state.astype(np.float32), {}
 
     def step(self, action):
+        t0 = self._v.sim.times()[0]           # current_time before the step: the ON grid's length
+        p = self.params_dict
+        self._n_on = len(np.arange(t0, t0 + p["electrode_width"], p["verbose_dt"]))   # env.py:426-428
         obs, rew, term, trunc, info = self._v.step(np.asarray(action, np.float32).reshape(1, -1))
         self.current_step += 1
         self.done = bool(term[0].item())
@@ -611,6 +631,28 @@ class SpatialKuramoto:
         """Every saved phase row of the last step, ys_I then ys_II (env.py:430,440): (nsamp + 1, N) float32."""
         n = int(self._v.sim.nsamp[0].item())
         return self._v.sim.rows[0, :n + 1].cpu().numpy()
+
+    @property
+    def sol_state(self):
+        """The last solve's rows (env.py:429,439): after step(), the stim-OFF
+        solve's ys_II (sol_state_ from the duplicated I/II boundary row on).
+        After reset() the reference holds the transient's 4000 rows, which
+        the library does not keep (only its last row, the state): raises
+        AttributeError until the first step."""
+        if getattr(self, "_n_on", None) is None:
+            raise AttributeError("sol_state after reset() would be the transient's 4000 rows (env.py:610), which "
+                                 "are not kept; step() first, or read the state (its last row) with "
+                                 "get_state()['y']")
+        return self.sol_state_[self._n_on:]
+
+    @property
+    def init_state(self):
+        """theta0 of the last reset (env.py:594-598), float64."""
+        return self._v.get_attr("init_state")[0]
+
+    @property
+    def theta_record_transient(self):
+        raise AttributeError(_UNSERVED["theta_record_transient"])
 
     def _reward(self, kind, x_state, action_value):
         """Any 1-D length (the bins follow len(x_state), utils.py:21-27)."""

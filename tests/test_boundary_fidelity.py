@@ -47,4 +47,17 @@ def test_single_env_sol_state_rows():
             assert n == env.theta_mean[s] and r == env.theta_records[s], (k, s)
     # the duplicate row: ys_II[0] == ys_I[-1]; find it as two equal consecutive rows
     assert any(np.array_equal(rows[i], rows[i + 1]) for i in range(2, 5))
+    # sol_state (env.py:439) = ys_II: starts at the duplicated boundary row, ends at the state
+    ys2 = env.sol_state
+    assert np.array_equal(ys2[0], rows[len(rows) - len(ys2) - 1]) and np.array_equal(ys2[-1], rows[-1])
+    assert len(ys2) in (15, 16)
+    # init_state (env.py:594-598): the last reset's theta0 draws, float64
+    th0 = env.init_state
+    assert th0.dtype == np.float64 and th0.shape == (env._v.N,)
+    env.reset()
+    assert not np.array_equal(th0, env.init_state)
+    with pytest.raises(AttributeError, match="transient"):
+        env.sol_state
+    with pytest.raises(AttributeError, match="3999"):
+        env.theta_record_transient
     env.close()
