@@ -431,6 +431,11 @@ struct CtlE {
     int keep, nsave;          // decision of the last attempted step
     int acc_steps, acc_rej;   // over the solves of one launch (stats)
     float t1, tprev, tnext, h, dtn;
+    // post_step decides and advances time in one section (before the saves
+    // of the step): the save passes read the step's save index and
+    // interval from here
+    int sv_si;
+    float sv_tprev, sv_tnext;
 };
 __shared__ CtlE s_ctl[E_WG];
 __shared__ float s_kn[E_WG];  // per-env coupling gain of the workgroup's envs
@@ -441,7 +446,6 @@ __shared__ double s_redd[RC][NWAVES][E_WG];      // per-wave partial sums (f64, 
 __shared__ float s_theta[E_WG][RC_N];            // dense-output abscissae of the rounds of a pass
 __shared__ int s_rflag[E_WG][RC_N];              // bit0: save row, bit1: LFP row, bit2: final row
 __shared__ double s_u[E_WG][4];                  // rescaled amplitudes (env.py:389-393)
-__shared__ int s_maxsave, s_any, s_fsal;
 __shared__ int s_nI[E_WG], s_nII[E_WG];          // ON / OFF grid lengths of the step (step_pair)
 
 __device__ __forceinline__ double grid_at_c(const CtlE& c, int i) {
@@ -909,12 +913,133 @@ __device__ __forceinline__ const float* group_publish_x(const DevParams& p, Part
     return p.xg + img;
 }
 
+// The error estimate and dense-output coefficients of one tile of the step
+// just taken (diffrax Dopri5: Shampine error weights kE, 4th-order
+// interpolation c_mid weights kM; oracle solve()): part[q] += (err/scale)^2,
+// CA/CB/CC records stored.  k_j = h f_j.
+template <typename DP>
+__device__ __forceinline__ void err_dense_tile(const DP& p, const Slot& ws, int t, const float (&h)[8],
+                                               const float (&y0)[8], const float (&y1)[8], const float (&f0)[8],
+                                               const float (&f2)[8], const float (&f3)[8], const float (&f4)[8],
+                                               const float (&f5)[8], const float (&f6)[8], float (&part)[8]) {
+    float ca[8], cb[8], cc[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        const float k0 = h[q] * f0[q], k2 = h[q] * f2[q], k3 = h[q] * f3[q], k4 = h[q] * f4[q],
+                    k5 = h[q] * f5[q], k6 = h[q] * f6[q];
+        float er = kE[0] * k0;
+        er = __builtin_fmaf(kE[2], k2, er);
+        er = __builtin_fmaf(kE[3], k3, er);
+        er = __builtin_fmaf(kE[4], k4, er);
+        er = __builtin_fmaf(kE[5], k5, er);
+        er = __builtin_fmaf(kE[6], k6, er);
+        const float a0 = fabsf(y0[q]), a1 = fabsf(y1[q]);
+        const float mx = a0 > a1 ? a0 : a1;
+        const float den = p.atol + mx * p.rtol;
+        const float qe = er / den;
+        part[q] = part[q] + qe * qe;
+        float acc = kM[0] * k0;
+        acc = __builtin_fmaf(kM[2], k2, acc);
+        acc = __builtin_fmaf(kM[3], k3, acc);
+        acc = __builtin_fmaf(kM[4], k4, acc);
+        acc = __builtin_fmaf(kM[5], k5, acc);
+        acc = __builtin_fmaf(kM[6], k6, acc);
+        const float yy0 = y0[q], yy1 = y1[q];
+        const float ym = yy0 + acc;
+        ca[q] = ((2.0f * (k6 - k0)) - (8.0f * (yy1 + yy0))) + (16.0f * ym);
+        cb[q] = ((((5.0f * k0) - (3.0f * k6)) + (18.0f * yy0)) + (14.0f * yy1)) - (32.0f * ym);
+        cc[q] = (((k6 - (4.0f * k0)) - (11.0f * yy0)) - (5.0f * yy1)) + (16.0f * ym);
+    }
+    store8(ws, SL_CA, t, ca);
+    store8(ws, SL_CB, t, cb);
+    store8(ws, SL_CC, t, cc);
+}
+
+// Stage 6 (the last sweep of a Dopri step): the coupling epilogue fused with
+// post_step's error pass -- f6 goes from the accumulators into the error
+// estimate and dense-output coefficients of its tile without a round trip
+// through its record, and the partials are published before the epilogue's
+// own barrier, which then also orders them (one pass and one barrier less
+// per Dopri step).  Same operations, same order as the two passes.
+template <int TPW, bool XL>
+__device__ __forceinline__ void coupling_epilogue_err(const DevParams& __restrict__ p, const Slot& ws,
+                                                      const float* __restrict__ Xs, const float* __restrict__ xown,
+                                                      const floatx16 (&acc)[TPW], bool pulse_on) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    float knq[8], h[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        knq[q] = s_kn[mfma_env(q, lane)];
+        h[q] = s_ctl[mfma_env(q, lane)].h;
+    }
+    float part[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int t = 0; t < TPW; ++t) {
+        float w[8], u[8];
+        load8(ws, SL_W, t, w);
+        if (pulse_on) {
+            load8(ws, SL_P, t, u);
+        } else {
+#pragma unroll
+            for (int q = 0; q < 8; ++q) u[q] = 0.0f;  // still added: x + 0 is not folded (signed zeros)
+        }
+        float y0[8], y1[8], f0[8], f2[8], f3[8], f4[8], f5[8];
+        load8(ws, SL_Y0, t, y0);
+        load8(ws, SL_Y1, t, y1);
+        load8(ws, SL_F0 + 0, t, f0);
+        load8(ws, SL_F0 + 2, t, f2);
+        load8(ws, SL_F0 + 3, t, f3);
+        load8(ws, SL_F0 + 4, t, f4);
+        load8(ws, SL_F0 + 5, t, f5);
+        const int i = 32 * (wave * TPW + t) + (lane & 31);
+        float f[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const int e = mfma_env(q, lane);
+            const float P = acc[t][q], Q = acc[t][q + 8];
+            float sn, cs;
+            if constexpr (XL) {
+                sn = xown[xs_idx(e, i)];
+                cs = xown[xs_idx(16 + e, i)];
+            } else {
+                sn = Xs[xs_idx(e, i)];
+                cs = Xs[xs_idx(16 + e, i)];
+            }
+            const float tq = sn * Q;
+            const float coup = __builtin_fmaf(cs, P, -tq);
+            f[q] = __builtin_fmaf(knq[q], coup, w[q]) + u[q];
+        }
+        store8(ws, SL_F0 + 6, t, f);
+        err_dense_tile(p, ws, t, h, y0, y1, f0, f2, f3, f4, f5, f, part);
+    }
+    rm_publish(part, 0);
+}
+
 // After the 7th stage: error norm, accept/reject, dense-output saves with
 // LFP, FSAL -- for all 16 envs, every wave on its own columns.
 // One pass of post_step's saves: rounds r0 .. r0+nk-1 (nk = min(RCX, nrounds - r0))
 // evaluated from the dense-output records of every tile, LFP partials reduced
 // in RM order, samples stored by thread e.  RCX is a compile-time bound on the
 // rounds of a pass (register arrays); rounds past nk are skipped.
+// Rounds r0 == 0 (the first pass) take their abscissae from post_step's
+// decision section (save_rounds_setup), later passes form them here.
+template <int RCX>
+__device__ __forceinline__ void save_rounds_setup(const CtlE& c, int e, int r0) {
+    for (int k = 0; k < RCX; ++k) {
+        const int r = r0 + k;
+        int fl = 0;
+        float th = 0.0f;
+        if (r < c.nsave) {
+            const int si = c.sv_si + r;
+            const float ts = (float)grid_at_c(c, si);
+            th = (ts - c.sv_tprev) / (c.sv_tnext - c.sv_tprev);
+            fl = 1 | ((si >= c.lfp_from && si < c.lfp_to) ? 2 : 0) | ((si == c.n - 1) ? 4 : 0);
+        }
+        s_theta[e][k] = th;
+        s_rflag[e][k] = fl;
+    }
+}
+
 template <int TPW, bool XL, int RCX>
 __device__ __forceinline__ void save_pass(const DevParams& __restrict__ p, const Slot& ws, int env_base, bool to_ring, Part& pt,
                                           const float (&h)[8], int r0, int nrounds, bool gauss STAMP_PARAMS) {
@@ -926,23 +1051,26 @@ __device__ __forceinline__ void save_pass(const DevParams& __restrict__ p, const
     // per-round flag bits, 3 per round: LFP rows, and LFP or final rows
     constexpr int kLfp = (int)(02222222222u & ((1u << (3 * RCX)) - 1u));
     constexpr int kEval = (int)(06666666666u & ((1u << (3 * RCX)) - 1u));
-    // (1) abscissa and flags of every (env, round) of the pass: one thread each
-    if (tid < E_WG * RCX) {
-        const int e = tid % E_WG, k = tid / E_WG;
-        const CtlE& c = s_ctl[e];
-        const int r = r0 + k;
-        int fl = 0;
-        float th = 0.0f;
-        if (r < c.nsave) {
-            const int si = c.si + r;
-            const float ts = (float)grid_at_c(c, si);
-            th = (ts - c.tprev) / (c.tnext - c.tprev);
-            fl = 1 | ((si >= c.lfp_from && si < c.lfp_to) ? 2 : 0) | ((si == c.n - 1) ? 4 : 0);
+    // (1) abscissa and flags of every (env, round) of the pass: one thread
+    // each (the first pass's were formed in post_step's decision section)
+    if (r0 > 0) {
+        if (tid < E_WG * RCX) {
+            const int e = tid % E_WG, k = tid / E_WG;
+            const CtlE& c = s_ctl[e];
+            const int r = r0 + k;
+            int fl = 0;
+            float th = 0.0f;
+            if (r < c.nsave) {
+                const int si = c.sv_si + r;
+                const float ts = (float)grid_at_c(c, si);
+                th = (ts - c.sv_tprev) / (c.sv_tnext - c.sv_tprev);
+                fl = 1 | ((si >= c.lfp_from && si < c.lfp_to) ? 2 : 0) | ((si == c.n - 1) ? 4 : 0);
+            }
+            s_theta[e][k] = th;
+            s_rflag[e][k] = fl;
         }
-        s_theta[e][k] = th;
-        s_rflag[e][k] = fl;
+        lds_barrier();
     }
-    lds_barrier();
     STAMP(11);
     float th[RCX][8];
     int fl[8];
@@ -987,7 +1115,7 @@ __device__ __forceinline__ void save_pass(const DevParams& __restrict__ p, const
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
             const CtlE& c = s_ctl[mfma_env(q, lane)];
-            rbase[q] = c.si + r0 - c.lfp_from + c.pos0;
+            rbase[q] = c.sv_si + r0 - c.lfp_from + c.pos0;
         }
     }
     // (2) dense output + LFP partials: every (round, env) of a tile is
@@ -1162,7 +1290,7 @@ __device__ __forceinline__ void save_pass(const DevParams& __restrict__ p, const
                 const CtlE& c = s_ctl[e];
                 const float ln = rm_total(e, k) / (float)NG;
                 const double lr = gauss ? 0.0 + rm_total_d(e, k) / (double)NG : (double)ln;
-                const int pos = c.si + r0 + k - c.lfp_from + c.pos0;
+                const int pos = c.sv_si + r0 + k - c.lfp_from + c.pos0;
                 KDBG_CHECK(p.stats, pos >= 0 && (to_ring ? pos < p.W : pos < KURA_S_MAX + 2) && env_base + e < p.B);
                 if (to_ring) {
                     p.ring[(size_t)(env_base + e) * p.W + pos] = lr;
@@ -1189,7 +1317,7 @@ __device__ __forceinline__ void save_pass(const DevParams& __restrict__ p, const
             const CtlE& c = s_ctl[tid];
             for (int k = 0; k < RCX; ++k) {
                 if (!(s_rflag[tid][k] & 2)) continue;
-                const int si = c.si + r0 + k;
+                const int si = c.sv_si + r0 + k;
                 const float ln = ltot[k] / (float)NG;
                 const double lr = gauss ? 0.0 + ltot_d[k] / (double)NG : (double)ln;
                 const int pos = si - c.lfp_from + c.pos0;
@@ -1203,19 +1331,24 @@ __device__ __forceinline__ void save_pass(const DevParams& __restrict__ p, const
             }
         }
     }
-    lds_barrier();
+    // the next pass rewrites s_theta / s_rflag / s_red; after the last pass
+    // nothing reads them before post_step's next barriers
+    if (XL || r0 + RCX < nrounds) lds_barrier();
     STAMP(15);
 }
 
+// Returns whether any env of the workgroup goes on integrating (uniform).
 template <int TPW, bool XL>
-__device__ __forceinline__ void post_step(const DevParams& __restrict__ p, Slot& ws, int env_base, bool to_ring, Part& pt
-                                          STAMP_PARAMS) {
+__device__ __forceinline__ int post_step(const DevParams& __restrict__ p, Slot& ws, int env_base, bool to_ring, Part& pt
+                                         STAMP_PARAMS) {
     const int lane = threadIdx.x & 63, tid = threadIdx.x;
     const int NG = XL ? __builtin_amdgcn_readfirstlane(pt.ng) : TPW * 256;   // oscillators per env
     float h[8];
 #pragma unroll
     for (int q = 0; q < 8; ++q) h[q] = s_ctl[mfma_env(q, lane)].h;
-    // (1) scaled error partials and dense-output coefficients
+#ifdef KURA_UNFUSED_ERR
+    // (1) scaled error partials and dense-output coefficients (A/B form: a
+    // pass of its own; by default it is fused into the stage-6 epilogue)
     float part[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll 1
     for (int t = 0; t < TPW; ++t) {
@@ -1228,51 +1361,32 @@ __device__ __forceinline__ void post_step(const DevParams& __restrict__ p, Slot&
         load8(ws, SL_F0 + 4, t, f4);
         load8(ws, SL_F0 + 5, t, f5);
         load8(ws, SL_F0 + 6, t, f6);
-        float ca[8], cb[8], cc[8];
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-            const float k0 = h[q] * f0[q], k2 = h[q] * f2[q], k3 = h[q] * f3[q], k4 = h[q] * f4[q],
-                        k5 = h[q] * f5[q], k6 = h[q] * f6[q];
-            float er = kE[0] * k0;
-            er = __builtin_fmaf(kE[2], k2, er);
-            er = __builtin_fmaf(kE[3], k3, er);
-            er = __builtin_fmaf(kE[4], k4, er);
-            er = __builtin_fmaf(kE[5], k5, er);
-            er = __builtin_fmaf(kE[6], k6, er);
-            const float a0 = fabsf(y0[q]), a1 = fabsf(y1[q]);
-            const float mx = a0 > a1 ? a0 : a1;
-            const float den = p.atol + mx * p.rtol;
-            const float qe = er / den;
-            part[q] = part[q] + qe * qe;
-            float acc = kM[0] * k0;
-            acc = __builtin_fmaf(kM[2], k2, acc);
-            acc = __builtin_fmaf(kM[3], k3, acc);
-            acc = __builtin_fmaf(kM[4], k4, acc);
-            acc = __builtin_fmaf(kM[5], k5, acc);
-            acc = __builtin_fmaf(kM[6], k6, acc);
-            const float yy0 = y0[q], yy1 = y1[q];
-            const float ym = yy0 + acc;
-            ca[q] = ((2.0f * (k6 - k0)) - (8.0f * (yy1 + yy0))) + (16.0f * ym);
-            cb[q] = ((((5.0f * k0) - (3.0f * k6)) + (18.0f * yy0)) + (14.0f * yy1)) - (32.0f * ym);
-            cc[q] = (((k6 - (4.0f * k0)) - (11.0f * yy0)) - (5.0f * yy1)) + (16.0f * ym);
-        }
-        store8(ws, SL_CA, t, ca);
-        store8(ws, SL_CB, t, cb);
-        store8(ws, SL_CC, t, cc);
+        err_dense_tile(p, ws, t, h, y0, y1, f0, f2, f3, f4, f5, f6, part);
     }
     rm_publish(part, 0);
     STAMP(5);
     lds_barrier();
+#endif
+    // (the scaled error partials of every wave are in s_red[0], behind the
+    // stage-6 epilogue's barrier)
     float etot[1] = {tid < E_WG ? rm_total(tid, 0) : 0.0f};
     if constexpr (XL) {
         double dummy[1] = {0.0};
         group_sum<1>(p, pt, etot, dummy, 1, false);
     }
-    // (2) thread e: accept/reject, step-size update (diffrax PIDController)
+    // (2) thread e: accept/reject, step-size update (diffrax PIDController),
+    // then at once the time advance (adapt_step_size + _clip_to_end) and the
+    // next step size; the saves below read the step's save index and
+    // interval from the sv_* snapshot, and the first save pass's abscissae
+    // are formed here too (one section and barrier instead of four)
+    const bool gauss = p.rec_kernel == KURA_REC_GAUSSIAN;
     if (tid < E_WG) {
         CtlE& c = s_ctl[tid];
         c.nsave = 0;
         c.keep = 0;
+        c.sv_si = c.si;
+        c.sv_tprev = c.tprev;
+        c.sv_tnext = c.tnext;
         const float mean = etot[0] / (float)NG;
         if (c.active && !(mean <= 3.40282346638528859812e+38f)) {
             // non-finite state or RHS (NaN/Inf reaches the error norm): the
@@ -1295,30 +1409,47 @@ __device__ __forceinline__ void post_step(const DevParams& __restrict__ p, Slot&
                 c.nsave = k;
             }
         }
-    }
-    lds_barrier();
-    if (tid == 0) {
-        // most save rounds of any env; FSAL mode: 0 no active env accepts
-        // (nothing to move), 2 every active env accepts (rename the slot
-        // pairs), 1 mixed (select-copy)
-        int m = 0, allk = 1, anyk = 0;
-        for (int e = 0; e < E_WG; ++e) {
-            const CtlE& c = s_ctl[e];
-            m = c.nsave > m ? c.nsave : m;
-            if (c.active) {
-                allk &= c.keep;
-                anyk |= c.keep;
+        if (c.active) {  // time advance (formerly after the saves)
+            c.si += c.nsave;
+            if (c.keep) c.tprev = c.tnext;
+            else c.rejected++;
+            float tn = c.tprev + c.dtn;
+            c.tprev = fminf(c.tprev, c.t1);
+            if (tn > c.t1 - 1e-6f) tn = c.keep ? c.t1 : c.tprev + 0.5f * (c.t1 - c.tprev);
+            c.tnext = tn;
+            c.nsteps++;
+            if (!(c.tprev < c.t1)) c.active = 0;
+            if (c.active && c.nsteps >= p.max_steps) {
+                c.flags |= KURA_F_MAX_STEPS;
+                c.active = 0;
             }
+            if (c.active) c.h = c.tnext - c.tprev;   // the next attempt's step
         }
-        s_maxsave = m;
-        s_fsal = anyk ? (allk ? 2 : 1) : 0;
+        if (XL || gauss) save_rounds_setup<RC>(c, tid, 0);
+        else save_rounds_setup<RC_N>(c, tid, 0);
     }
     lds_barrier();
+    // every wave: most save rounds of any env; FSAL mode: 0 no env that goes
+    // on integrating accepts (nothing to move), 2 every such env accepts
+    // (rename the slot pairs), 1 mixed (select-copy) -- envs that end their
+    // solve with this step never read their records again; and whether any
+    // env goes on (the solve loop's exit).  Wave-uniform reads of s_ctl.
+    int nrounds = 0, allk = 1, anyk = 0, any = 0;
+#pragma unroll
+    for (int e = 0; e < E_WG; ++e) {
+        const CtlE& c = s_ctl[e];
+        const int ns = __builtin_amdgcn_readfirstlane(c.nsave);
+        const int ac = __builtin_amdgcn_readfirstlane(c.active), kp = __builtin_amdgcn_readfirstlane(c.keep);
+        nrounds = ns > nrounds ? ns : nrounds;
+        if (ac) {
+            allk &= kp;
+            anyk |= kp;
+            any = 1;
+        }
+    }
     STAMP(7);
-    const int nrounds = s_maxsave;
     // (3) saves: up to RCX rounds (save indices) per pass over the records,
     // all envs in parallel; one RM reduction per round and LFP kind
-    const bool gauss = p.rec_kernel == KURA_REC_GAUSSIAN;
     if (XL || gauss) {
 #pragma unroll 1
         for (int r0 = 0; r0 < nrounds; r0 += RC)
@@ -1335,7 +1466,7 @@ __device__ __forceinline__ void post_step(const DevParams& __restrict__ p, Slot&
     int kp[8];
 #pragma unroll
     for (int q = 0; q < 8; ++q) kp[q] = s_ctl[mfma_env(q, lane)].keep;
-    const int fmode = __builtin_amdgcn_readfirstlane(s_fsal);
+    const int fmode = anyk ? (allk ? 2 : 1) : 0;
     if (fmode == 2) ws.par ^= 1;
 #pragma unroll 1
     for (int t = 0; t < (fmode == 1 ? TPW : 0); ++t) {
@@ -1353,33 +1484,22 @@ __device__ __forceinline__ void post_step(const DevParams& __restrict__ p, Slot&
         store8(ws, SL_F0, t, f0);
     }
     STAMP(9);
-    // (5) thread e: time advance (adapt_step_size + _clip_to_end)
-    lds_barrier();
-    if (tid < E_WG) {
-        CtlE& c = s_ctl[tid];
-        if (c.active) {
-            c.si += c.nsave;
-            if (c.keep) c.tprev = c.tnext;
-            else c.rejected++;
-            float tn = c.tprev + c.dtn;
-            c.tprev = fminf(c.tprev, c.t1);
-            if (tn > c.t1 - 1e-6f) tn = c.keep ? c.t1 : c.tprev + 0.5f * (c.t1 - c.tprev);
-            c.tnext = tn;
-            c.nsteps++;
-            if (!(c.tprev < c.t1)) c.active = 0;
-            if (c.active && c.nsteps >= p.max_steps) {
-                c.flags |= KURA_F_MAX_STEPS;
-                c.active = 0;
-            }
-        }
-    }
-    lds_barrier();
+    // no barrier here: nothing the saves / FSAL wrote (records: per lane; ring,
+    // LFP samples: thread e) is read by another thread before the next
+    // stage's barrier, and the next stage input only writes the operand,
+    // whose last readers (the stage-6 GEMM and epilogue) are behind a barrier
+    return any;
 }
 
 // One diffeqsolve for the workgroup's 16 envs.  s_ctl must be initialised
 // (ctl_begin) and visible before the call.
+#ifdef KURA_SOLVE_NOINLINE   // A/B: the solver as a called function (a call frame per solve)
+#define KURA_SOLVE_ATTR __noinline__
+#else
+#define KURA_SOLVE_ATTR __forceinline__
+#endif
 template <int TPW, bool XL>
-__device__ void solve_wg(const DevParams& __restrict__ p, float* Xs, int env_base, bool to_ring, bool pulse_on,
+__device__ KURA_SOLVE_ATTR void solve_wg(const DevParams& __restrict__ p, float* Xs, int env_base, bool to_ring, bool pulse_on,
                          long long* rhs_count, Part& pt) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, tid = threadIdx.x;
     constexpr int N = TPW * 256;            // oscillators owned by this workgroup
@@ -1435,7 +1555,11 @@ __device__ void solve_wg(const DevParams& __restrict__ p, float* Xs, int env_bas
 #endif
         }
         STAMP(2);
-        coupling_epilogue<TPW, XL>(p, ws, Xs, xown, acc, s, pulse_on);
+#ifndef KURA_UNFUSED_ERR
+        if (s == 6) coupling_epilogue_err<TPW, XL>(p, ws, Xs, xown, acc, pulse_on);
+        else
+#endif
+            coupling_epilogue<TPW, XL>(p, ws, Xs, xown, acc, s, pulse_on);
         STAMP(3);
         lds_barrier();  // every wave is done reading the operand before it is rewritten
         STAMP(4);
@@ -1446,20 +1570,19 @@ __device__ void solve_wg(const DevParams& __restrict__ p, float* Xs, int env_bas
             STAMP(0);
             continue;
         }
+        int any;
         if (s == 6) {
-            post_step<TPW, XL>(p, ws, env_base, to_ring, pt STAMP_ARGS);
+            any = post_step<TPW, XL>(p, ws, env_base, to_ring, pt STAMP_ARGS);   // advances time, sets h
             STAMP(10);
+        } else {  // the solve's initial sweep: the first attempt's step size
+            if (tid < E_WG && s_ctl[tid].active) s_ctl[tid].h = s_ctl[tid].tnext - s_ctl[tid].tprev;
+            any = 0;
+#pragma unroll
+            for (int e = 0; e < E_WG; ++e) any |= __builtin_amdgcn_readfirstlane(s_ctl[e].active);
+            lds_barrier();
+            STAMP(6);
         }
-        if (tid == 0) {
-            int any = 0;
-            for (int e = 0; e < E_WG; ++e) any |= s_ctl[e].active;
-            s_any = any;
-            for (int e = 0; e < E_WG; ++e)
-                if (s_ctl[e].active) s_ctl[e].h = s_ctl[e].tnext - s_ctl[e].tprev;
-        }
-        lds_barrier();
-        STAMP(6);
-        if (s_any == 0) break;
+        if (any == 0) break;
         // stage 1 of the next Dopri step (f_0: the stage-0 record, or the
         // FSAL select of post_step)
         s = 1;
@@ -1766,30 +1889,36 @@ __device__ __forceinline__ void step_pair(const DevParams& p, Part& pt, float* X
     }
     __syncthreads();
     long long rhs = 0;
-    solve_wg<TPW, XL>(p, Xs, env_base, false, true, &rhs, pt);
-    __syncthreads();  // global stores of the solve (y) before the OFF setup
-    // ---- stimulation OFF (env.py:433-441)
-    if (tid < E_WG) {
-        CtlE& c = s_ctl[tid];
-        const int env = env_base + tid;
-        c.active = 0;
-        if (env < p.B && !c.flags) {
-            const int nI = s_nI[tid];
-            const double tm = grid_at_c(c, nI - 1);
-            const Grid g = make_grid(tm, tm + p.pause, p.dt);
-            s_nII[tid] = g.n;
-            ctl_begin(c, g, p.dt0, 1, g.n - 1, nI + 1);
-            if (g.n < 2 || nI + g.n - 1 > KURA_S_MAX) {
+    // the stim-ON solve, then the stim-OFF solve: one call site of the
+    // (inlined) solver, so the kernel carries no call frame for it
+#pragma unroll 1
+    for (int ph = 0; ph < 2; ++ph) {
+        if (ph == 1) {
+            __syncthreads();  // global stores of the solve (y) before the OFF setup
+            // ---- stimulation OFF (env.py:433-441)
+            if (tid < E_WG) {
+                CtlE& c = s_ctl[tid];
+                const int env = env_base + tid;
                 c.active = 0;
-                c.flags |= KURA_F_GRID;
-            } else {  // ys_II[0] == ys_I[-1]: duplicated sample (env.py:440)
-                s_smp_n[tid][nI] = s_smp_n[tid][nI - 1];
-                s_smp_r[tid][nI] = s_smp_r[tid][nI - 1];
+                if (env < p.B && !c.flags) {
+                    const int nI = s_nI[tid];
+                    const double tm = grid_at_c(c, nI - 1);
+                    const Grid g = make_grid(tm, tm + p.pause, p.dt);
+                    s_nII[tid] = g.n;
+                    ctl_begin(c, g, p.dt0, 1, g.n - 1, nI + 1);
+                    if (g.n < 2 || nI + g.n - 1 > KURA_S_MAX) {
+                        c.active = 0;
+                        c.flags |= KURA_F_GRID;
+                    } else {  // ys_II[0] == ys_I[-1]: duplicated sample (env.py:440)
+                        s_smp_n[tid][nI] = s_smp_n[tid][nI - 1];
+                        s_smp_r[tid][nI] = s_smp_r[tid][nI - 1];
+                    }
+                }
             }
+            __syncthreads();
         }
+        solve_wg<TPW, XL>(p, Xs, env_base, false, ph == 0, &rhs, pt);
     }
-    __syncthreads();
-    solve_wg<TPW, XL>(p, Xs, env_base, false, false, &rhs, pt);
     STAMP_DECL  // diagnostic build: the tail's phases in slots 20-22
     __syncthreads();
     // ---- window, reward, outputs (env.py:443-454): wave w owns envs 2w, 2w+1

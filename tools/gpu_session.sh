@@ -20,13 +20,17 @@ if [ "$TESTS" != "none" ]; then
   [ $rc -eq 0 ] || [ $rc -eq 1 ] || { echo "tests rc=$rc"; exit $rc; }
 fi
 IFS=';' read -ra SETV <<< "$SETS"
-for round in 1 2; do
+for round in $(seq 1 ${ROUNDS:-2}); do
   for tree in "$@"; do
-    tn=$(basename $(cd $tree && pwd)); [ "$tree" = "." ] && tn=head
+    # "lib:<path>": this tree with another build of libkura (KURA_LIB)
+    lib=""; t=$tree
+    case $tree in lib:*) lib=${tree#lib:}; t=.;; esac
+    tn=$(basename $(cd $t && pwd)); [ "$t" = "." ] && tn=head
+    [ -n "$lib" ] && tn=$(basename $lib .so)
     si=0
     for set in "${SETV[@]}"; do
       f=$O/bench_${tn}_${si}_${round}.json
-      (cd $tree && timeout -k 10 300 python3 bench.py $set --cpu-seconds 0 > $f 2> ${f%.json}.err) || { echo "bench $tn [$set] failed"; exit 1; }
+      (cd $t && KURA_LIB=${lib:+$R/$lib} timeout -k 10 300 python3 bench.py $set --cpu-seconds 0 > $f 2> ${f%.json}.err) || { echo "bench $tn [$set] failed"; exit 1; }
       python3 -c "import json,sys;d=json.loads([l for l in open('$f') if l.startswith('{')][-1]);print('$tn','[$set]','r$round',round(d['value']),round(d['ms_per_step'],4),round(d['roofline']['frac'],4),round(d['roofline']['avg_kernel_ms'],4),round(d['extra'].get('reset_ms',0),1))" | tee -a $O/summary.txt
       si=$((si+1))
     done
