@@ -955,12 +955,13 @@ __device__ __forceinline__ void err_dense_tile(const DP& p, const Slot& ws, int 
     store8(ws, SL_CC, t, cc);
 }
 
-// Stage 6 (the last sweep of a Dopri step): the coupling epilogue fused with
+// A/B form (-DKURA_FUSED_ERR): stage 6's coupling epilogue fused with
 // post_step's error pass -- f6 goes from the accumulators into the error
 // estimate and dense-output coefficients of its tile without a round trip
 // through its record, and the partials are published before the epilogue's
 // own barrier, which then also orders them (one pass and one barrier less
-// per Dopri step).  Same operations, same order as the two passes.
+// per Dopri step).  Same operations, same order as the two passes; measured
+// 2 % slower than the separate passes, so not the default.
 template <int TPW, bool XL>
 __device__ __forceinline__ void coupling_epilogue_err(const DevParams& __restrict__ p, const Slot& ws,
                                                       const float* __restrict__ Xs, const float* __restrict__ xown,
@@ -1346,9 +1347,12 @@ __device__ __forceinline__ int post_step(const DevParams& __restrict__ p, Slot& 
     float h[8];
 #pragma unroll
     for (int q = 0; q < 8; ++q) h[q] = s_ctl[mfma_env(q, lane)].h;
-#ifdef KURA_UNFUSED_ERR
-    // (1) scaled error partials and dense-output coefficients (A/B form: a
-    // pass of its own; by default it is fused into the stage-6 epilogue)
+#ifndef KURA_FUSED_ERR
+    // (1) scaled error partials and dense-output coefficients: a pass of its
+    // own.  (-DKURA_FUSED_ERR folds it into the stage-6 epilogue instead:
+    // one record round trip and one barrier less per Dopri step, yet 2 %
+    // slower in the same-box A/B -- the fused epilogue holds the
+    // accumulators and the seven records of a tile at once)
     float part[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll 1
     for (int t = 0; t < TPW; ++t) {
@@ -1367,8 +1371,8 @@ __device__ __forceinline__ int post_step(const DevParams& __restrict__ p, Slot& 
     STAMP(5);
     lds_barrier();
 #endif
-    // (the scaled error partials of every wave are in s_red[0], behind the
-    // stage-6 epilogue's barrier)
+    // (KURA_FUSED_ERR: the scaled error partials of every wave are in
+    // s_red[0], behind the stage-6 epilogue's barrier)
     float etot[1] = {tid < E_WG ? rm_total(tid, 0) : 0.0f};
     if constexpr (XL) {
         double dummy[1] = {0.0};
@@ -1493,10 +1497,15 @@ __device__ __forceinline__ int post_step(const DevParams& __restrict__ p, Slot& 
 
 // One diffeqsolve for the workgroup's 16 envs.  s_ctl must be initialised
 // (ctl_begin) and visible before the call.
-#ifdef KURA_SOLVE_NOINLINE   // A/B: the solver as a called function (a call frame per solve)
-#define KURA_SOLVE_ATTR __noinline__
-#else
+// The solver is a called function (one call site per kernel; its frame saves
+// the callee-saved registers once per solve).  Inlined (-DKURA_SOLVE_INLINE)
+// the kernel needs less scratch (648 vs ~1200 B per lane for <4, false>) but
+// the register allocation of the combined body spills inside the sweep loop:
+// same-box A/B, 0.750 vs 0.788 of the FP32 MFMA peak.
+#ifdef KURA_SOLVE_INLINE
 #define KURA_SOLVE_ATTR __forceinline__
+#else
+#define KURA_SOLVE_ATTR __noinline__
 #endif
 template <int TPW, bool XL>
 __device__ KURA_SOLVE_ATTR void solve_wg(const DevParams& __restrict__ p, float* Xs, int env_base, bool to_ring, bool pulse_on,
@@ -1555,7 +1564,7 @@ __device__ KURA_SOLVE_ATTR void solve_wg(const DevParams& __restrict__ p, float*
 #endif
         }
         STAMP(2);
-#ifndef KURA_UNFUSED_ERR
+#ifdef KURA_FUSED_ERR
         if (s == 6) coupling_epilogue_err<TPW, XL>(p, ws, Xs, xown, acc, pulse_on);
         else
 #endif

@@ -546,6 +546,9 @@ class KuraVectorEnv:
                                   "kura_step (last call before close)")
 
 
+_SOL_STATE_AFTER_RESET = ("sol_state after reset() would be the transient's 4000 rows (env.py:610), which are not "
+                          "kept; step() first, or read the state (its last row) with get_state()['y']")
+
 # reference attributes the GPU path does not keep (no caller in the reference
 # reads them: aDBS_RL/, the notebooks); asking for them raises with the reason
 _UNSERVED = {
@@ -624,6 +627,11 @@ class SpatialKuramoto:
             raise AttributeError(name)
         if name in ("kw0", "kneur_grid", "kgrid_size") + KuraVectorEnv._HOST_ATTRS:
             return self._v.get_attr(name)[0]
+        # (a property that raises AttributeError lands here: keep its reason)
+        if name == "sol_state":
+            raise AttributeError(_SOL_STATE_AFTER_RESET)
+        if name in _UNSERVED:
+            raise AttributeError(_UNSERVED[name])
         raise AttributeError(f"'SpatialKuramoto' object has no attribute {name!r}")
 
     @property
@@ -640,9 +648,7 @@ class SpatialKuramoto:
         the library does not keep (only its last row, the state): raises
         AttributeError until the first step."""
         if getattr(self, "_n_on", None) is None:
-            raise AttributeError("sol_state after reset() would be the transient's 4000 rows (env.py:610), which "
-                                 "are not kept; step() first, or read the state (its last row) with "
-                                 "get_state()['y']")
+            raise AttributeError(_SOL_STATE_AFTER_RESET)
         return self.sol_state_[self._n_on:]
 
     @property

@@ -249,21 +249,22 @@ def test_reset_failure_runs_count_consecutive_failures_only(torch_gpu, monkeypat
     p = kura.reference_params("env0", "eval", 0)
     p["reward_func"] = "bbpow_action"
     p["total_episode_len"] = 2 * (p["electrode_width"] + p["electrode_pause"])   # 2-step episodes
+    orig = venv.reset_draws_batch
     for check in ("eager", "deferred"):
         env = venv.KuraVectorEnv(p, num_envs=2, on_failure="reset", max_reset_failures=1, failure_check=check)
         host = env.hosts[0]
-        orig = host.reset_draws
         calls = {"n": 0}
         poison = {1, 3}          # reset draws 1 and 3 of env 0 get a NaN phase (its transient fails)
 
-        def draws():
-            w0, gs, gr, th = orig()
-            calls["n"] += 1
-            if calls["n"] - 1 in poison:
-                th = th.copy()
-                th[0] = np.nan
+        def draws(hosts):
+            w0, gs, gr, th = orig(hosts)
+            for k, h in enumerate(hosts):
+                if h is host:
+                    if calls["n"] in poison:
+                        th[k, 0] = np.nan
+                    calls["n"] += 1
             return w0, gs, gr, th
-        monkeypatch.setattr(host, "reset_draws", draws)
+        monkeypatch.setattr(venv, "reset_draws_batch", draws)
         env.reset()                                            # draw 0: ok
         a = np.zeros((2, 1), np.float32)
         for _ in range(8):                                     # autoresets: draws 1 (fails), 2 (ok), 3 (fails), 4 ...
