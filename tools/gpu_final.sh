@@ -3,7 +3,7 @@
 # the default bench line (as the driver runs it), the --gpus 2 launcher
 # rehearsal on one device (gloo; default and env2 random-K shapes), the
 # N=8192 stress lines, the rocprofv3 trace + FETCH/WRITE/clock passes and the
-# SQ/SQC/TA counter passes.  Each step has its own time limit; the first
+# SQ/SQC/TA counter passes, and the phase stamps (KURA_STAMPS build).  Each step has its own time limit; the first
 # failure ends the script.
 #   bash tools/gpu_final.sh <tag> [quick]     (quick: skip the stress lines and counter passes)
 set -o pipefail
@@ -22,5 +22,6 @@ tail -2 $O/gpu_tests.log; cat $O/smoke.log | tail -1
 timeout -k 10 300 python3 bench.py --osc 8192 --envs 128 --steps 10 --warmup 2 --cpu-seconds 0 > $O/bench_stress128.json 2> $O/bench_stress128.err &&
 timeout -k 10 300 python3 bench.py --osc 8192 --envs 1024 --steps 4 --warmup 2 --cpu-seconds 0 > $O/bench_stress1024.json 2> $O/bench_stress1024.err &&
 bash tools/rocprof_run.sh ${T}_prof > $O/rocprof.log 2>&1 &&
-bash tools/pmc_pass.sh ${T}_pmc > $O/pmc.log 2>&1
+bash tools/pmc_pass.sh ${T}_pmc > $O/pmc.log 2>&1 &&
+timeout -k 10 300 python3 tools/phase_stamps.py > $O/stamps_step.json 2> $O/stamps_step.err
 echo "rc=$?"
