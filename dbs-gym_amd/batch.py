@@ -8,36 +8,76 @@ phases.  ``build_batch`` stacks B of them into the arrays libkura consumes.
 """
 from __future__ import annotations
 
+import functools
+import gc
 import os
 from copy import deepcopy
 
 import numpy as np
 
+from . import hostrng
 from . import model_setup as ms
 from .configs import STIM_REC_LOCUS
 
 
-class EnvHost:
-    """``rs``: the RandomState standing in for the reference's process-global
-    NumPy RNG.  By default each env owns one; pass a shared one to replay a
-    driver that constructs several envs in one process (it is reseeded here
-    with this env's rand_seed, as SpatialKuramoto.__init__ does, env.py:291)."""
+def _without_gc(fn):
+    """Batch setup allocates ~10 container objects per env and none of them
+    form cycles: the cyclic collector's passes over the growing heap were
+    ~0.2 s of a 4096-env setup, so it is paused for the call."""
+    @functools.wraps(fn)
+    def run(*a, **k):
+        on = gc.isenabled()
+        gc.disable()
+        try:
+            return fn(*a, **k)
+        finally:
+            if on:
+                gc.enable()
+    return run
 
-    def __init__(self, params: dict, rs: np.random.RandomState | None = None):
+
+def _own_stream(seed):
+    """The env's own RNG stream: a native MT19937 stream (hostrng.Stream, bit
+    for bit RandomState(seed)) for an integer seed in [0, 2**32), otherwise
+    numpy's RandomState itself (which accepts array seeds too)."""
+    if isinstance(seed, (int, np.integer)) and 0 <= int(seed) <= 0xFFFFFFFF:
+        return hostrng.StreamBank([int(seed)]).stream(0)
+    return np.random.RandomState(seed)
+
+
+def _copy_coords(c):
+    """deepcopy of a contact list ([[x, y, z], ...]) without copy.deepcopy's
+    per-object overhead."""
+    if isinstance(c, list) and all(isinstance(r, list) and all(isinstance(v, (int, float)) for v in r) for r in c):
+        return [list(r) for r in c]
+    return deepcopy(c)
+
+
+class EnvHost:
+    """``rs``: the RNG standing in for the reference's process-global NumPy
+    RNG.  By default each env owns a stream (``stream``: a row of a batch's
+    hostrng.StreamBank, already seeded with rand_seed; otherwise one is made);
+    pass a shared numpy RandomState as ``rs`` to replay a driver that
+    constructs several envs in one process (it is reseeded here with this
+    env's rand_seed, as SpatialKuramoto.__init__ does, env.py:291)."""
+
+    def __init__(self, params: dict, rs=None, stream=None):
         p = params
         self.p = p
-        if rs is None:
-            rs = np.random.RandomState(p["rand_seed"])                         # env.py:291
-        else:
+        if rs is not None:
             rs.seed(p["rand_seed"])
+        elif stream is not None:      # a row of a hostrng.StreamBank, seeded with rand_seed by the caller
+            rs = stream
+        else:
+            rs = _own_stream(p["rand_seed"])                                   # env.py:291
         self.rs = rs
         self.reset_count = -1
         self.N = int(p["num_oscillators"])
         self.grid = np.asarray(p["neur_grid"])
         self.w0_without_locus = np.array(p["w0_without_locus"], dtype=np.float64)
-        self.w0_without_locus_ = deepcopy(self.w0_without_locus)
-        self.elec_coords = deepcopy(p["elec_coords"])
-        self.rec_coords = deepcopy(p["rec_coords"])
+        self.w0_without_locus_ = self.w0_without_locus.copy()
+        self.elec_coords = _copy_coords(p["elec_coords"])
+        self.rec_coords = _copy_coords(p["rec_coords"])
         self.encapsulation_coeff = p["conduct_modifier"]                      # env.py:349
         # env.py:356-359 (logged when save_events; kept here always)
         self.temporal_events = {"electrode_drift": [], "encapsulation_drift": [], "plasticity_drift": [],
@@ -160,6 +200,12 @@ class EnvHost:
 _COND_CACHE: dict = {}   # (grid bytes, contacts, modifier, settings) -> read-only (g_stim, g_rec)
 
 
+def _check_w0(w0: np.ndarray) -> None:
+    if np.min(w0) < 0:
+        raise AssertionError("Natural frequencies w0 must be positive!")       # env.py:214
+
+
+@_without_gc
 def reset_draws_batch(hosts: list[EnvHost]):
     """EnvHost.reset_draws of several envs, bit-identical to one call per env
     (each env draws from its own stream, in the reference's order):
@@ -177,23 +223,46 @@ def reset_draws_batch(hosts: list[EnvHost]):
         h._advance_events()
     w0wo = np.stack([h.w0_without_locus for h in hosts])
     wl = np.stack([np.asarray(h.p["locus_without_w0"], np.float64) for h in hosts])
-    lm = np.stack([np.asarray(h.p["locus_mask"], np.float64) for h in hosts])
+    lm0 = hosts[0].p["locus_mask"] if hosts else None
+    if all(h.p["locus_mask"] is lm0 for h in hosts):
+        lm = np.asarray(lm0, np.float64)[None, :]            # one geometry (broadcast: same elementwise ops)
+    else:
+        lm = np.stack([np.asarray(h.p["locus_mask"], np.float64) for h in hosts])
     w0 = ms.apply_locus_mask(w0wo, wl, lm)                                      # env.py:566
-    neg = (w0 <= 0.).any(axis=1)
     th = np.empty_like(w0)
     gss, grs = [], []
+    banks: dict = {}     # id(bank) -> (bank, batch indices, bank rows)
     for k, h in enumerate(hosts):
-        if neg[k]:
-            w0[k] = ms.remove_negative_w0(h.rs, w0[k])                          # env.py:213
-            if np.min(w0[k]) < 0:
-                raise AssertionError("Natural frequencies w0 must be positive!")   # env.py:214
         g_stim, g_rec = h._conductances()
         gss.append(g_stim)
         grs.append(g_rec)
-        t = h.rs.normal(loc=h.p["init_state_mean"], scale=h.p["init_state_sd"], size=h.N)   # env.py:595-597
-        if (t <= 0.).any():
-            t = ms.remove_negative_w0(h.rs, t)                                  # env.py:598
-        th[k] = t
+        if isinstance(h.rs, hostrng.Stream):
+            b = banks.setdefault(id(h.rs.bank), (h.rs.bank, [], []))
+            b[1].append(k)
+            b[2].append(h.rs.row)
+        else:    # a (possibly shared) numpy RandomState: the reference's order, env by env
+            if (w0[k] <= 0.).any():
+                w0[k] = ms.remove_negative_w0(h.rs, w0[k])                      # env.py:213
+            _check_w0(w0[k])
+            t = h.rs.normal(loc=h.p["init_state_mean"], scale=h.p["init_state_sd"], size=h.N)   # env.py:595-597
+            if (t <= 0.).any():
+                t = ms.remove_negative_w0(h.rs, t)                              # env.py:598
+            th[k] = t
+    # the same draws for envs on their own native streams, each stream in the
+    # order above, one call per bank and draw (remove_negative_w0 draws only
+    # for rows with entries <= 0)
+    for bank, ks, rows in banks.values():
+        ks = np.asarray(ks)
+        wk = np.ascontiguousarray(w0[ks])
+        bank.remove_nonpositive(rows, wk)                                       # env.py:213
+        for r in wk:
+            _check_w0(r)
+        w0[ks] = wk
+        t = bank.normal(rows, [hosts[k].p["init_state_mean"] for k in ks],
+                        [hosts[k].p["init_state_sd"] for k in ks], th.shape[1])   # env.py:595-597
+        bank.remove_nonpositive(rows, t)                                        # env.py:598
+        th[ks] = t
+    for k, h in enumerate(hosts):
         h.w0 = w0[k]
     return w0, np.stack(gss), np.stack(grs), th
 
@@ -227,6 +296,7 @@ def fill_driver_arrays(params: dict, w0_seed: int | None = None, rs: np.random.R
     return p
 
 
+@_without_gc
 def fill_driver_arrays_batch(params_list: list[dict], w0_seeds) -> list[dict]:
     """fill_driver_arrays for many envs at once, bit-identical to calling it
     per env (tests/test_host.py): the grid, coordinates and locus mask are
@@ -241,12 +311,9 @@ def fill_driver_arrays_batch(params_list: list[dict], w0_seeds) -> list[dict]:
     if B == 0:
         return []
     geo = {}
-    rs = np.random.RandomState()
     N = int(params_list[0]["num_oscillators"])
-    rands = np.empty((B, N))
-    wls = np.empty((B, N))
     keys = []
-    for b, p in enumerate(params_list):
+    for p in params_list:
         if int(p["num_oscillators"]) != N:
             raise ValueError("fill_driver_arrays_batch: every env must have the same num_oscillators")
         key = (tuple(p["grid_size"]), float(p["coord_modif"]), tuple(p["locus_center"]), float(p["locus_size"]))
@@ -257,26 +324,47 @@ def fill_driver_arrays_batch(params_list: list[dict], w0_seeds) -> list[dict]:
                 a_.setflags(write=False)
             geo[key] = (coords, grid, lm)
         keys.append(key)
-        rs.seed(w0_seeds[b])
-        rands[b] = rs.rand(N)                                                    # sample_w0 (utils.py:868)
-        wls[b] = rs.uniform(low=p["wmuL"] - p["wsdL"], high=p["wmuL"] + p["wsdL"], size=N)   # utils.py:927
+    # each env's driver stream RandomState(w0_seeds[b]): rand(N) (sample_w0,
+    # utils.py:868) then uniform(N) (utils.py:927), all envs in two native calls
+    bank = hostrng.StreamBank(w0_seeds)
+    rows = np.arange(B)
+    rands = bank.random_sample(rows, N)
+    wls = bank.uniform(rows, [p["wmuL"] - p["wsdL"] for p in params_list],
+                       [p["wmuL"] + p["wsdL"] for p in params_list], N)
     w0_deg = ms.w0_from_uniform(rands)
+    # apply_locus_mask (utils.py:902-906) per geometry on the stacked rows
+    w = np.empty_like(w0_deg)
+    groups: dict = {}
+    for b, k in enumerate(keys):
+        groups.setdefault(k, []).append(b)
+    for k, bs in groups.items():
+        idx = np.asarray(bs)
+        w[idx] = ms.apply_locus_mask(w0_deg[idx], wls[idx], geo[k][2][None, :])
+    w *= 0.065
+    w0_deg *= 0.065
+    wls *= 0.065
     out = []
     for b, p in enumerate(params_list):
         coords, grid, lm = geo[keys[b]]
-        w = ms.apply_locus_mask(w0_deg[b], wls[b], lm)
         q = dict(p)
-        q.update(w0=w * 0.065, w0_without_locus=w0_deg[b] * 0.065, locus_without_w0=wls[b] * 0.065,
+        q.update(w0=w[b], w0_without_locus=w0_deg[b], locus_without_w0=wls[b],
                  locus_mask=lm, neur_coords=coords, neur_grid=grid)
         out.append(q)
     return out
 
 
+@_without_gc
 def build_batch(params_list: list[dict]) -> tuple[list[EnvHost], dict]:
     """Host setup for B envs sharing N, the grid and the spatial kernel: returns
     the EnvHost list and the shared coupling alpha (float64, env.py:219-229).
     K may differ per env (its float32(K/N) gain goes to kura_set_env_gain)."""
-    hosts = [EnvHost(p) for p in params_list]
+    # the envs' own streams (env.py:291 RandomState(rand_seed)) in one bank
+    ok = [isinstance(p["rand_seed"], (int, np.integer)) and 0 <= int(p["rand_seed"]) <= 0xFFFFFFFF
+          for p in params_list]
+    rows = np.cumsum(ok) - 1
+    bank = hostrng.StreamBank([int(p["rand_seed"]) for p, o in zip(params_list, ok) if o])
+    hosts = [EnvHost(p, stream=bank.stream(int(r)) if o else None)
+             for p, o, r in zip(params_list, ok, rows)]
     p0 = params_list[0]
     for p in params_list[1:]:
         if p["num_oscillators"] != p0["num_oscillators"] or list(p["grid_size"]) != list(p0["grid_size"]):
@@ -294,3 +382,4 @@ def reset_arrays(hosts: list[EnvHost], idx=None):
     idx = range(len(hosts)) if idx is None else idx
     w, gs, gr, th = reset_draws_batch([hosts[i] for i in idx])
     return w.astype(np.float32), gs, gr, th.astype(np.float32)
+

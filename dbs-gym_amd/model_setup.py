@@ -15,6 +15,8 @@ import numpy as np
 from scipy.integrate import quad
 from scipy.interpolate import interp1d
 
+from . import hostrng
+
 
 def neuron_grid_3d(gx: int, gy: int, gz: int, n: int, coord_modif: float = 0.1):
     """utils.py:478-497 generate_neuron_grid_3D (no shuffle).
@@ -123,7 +125,14 @@ def w0_from_uniform(u: np.ndarray) -> np.ndarray:
     global _INV_CDF
     if _INV_CDF is None:
         _INV_CDF = _w0_inverse_cdf()
-    return _INV_CDF(u)
+    f = _INV_CDF
+    u = np.asarray(u, dtype=np.float64)
+    if u.size < 4096:
+        return f(u)
+    # interp1d's linear path is numpy.interp on its sorted table with the fill
+    # values outside it; hostrng.interp is the same arithmetic, multithreaded
+    # (tests/test_hostrng.py checks it against f on the same draws)
+    return hostrng.interp(u, f.x, f.y, f.fill_value[0], f.fill_value[1]).reshape(u.shape)
 
 
 def sample_w0(rs: np.random.RandomState, n: int) -> np.ndarray:

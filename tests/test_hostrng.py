@@ -1,0 +1,137 @@
+"""libkura_host.so (dbs-gym_amd/csrc/kura_hostrng.c, hostrng.py): the native
+per-env MT19937 streams are bit for bit numpy.random.RandomState -- the
+reference's RNG (env.py:291, :595-598; utils.py:819-823, :868, :927) -- for
+every draw the host path makes, including the cached second Gaussian carried
+across calls, and the state tuples round-trip through get_state/set_state."""
+import importlib
+
+import numpy as np
+import pytest
+
+hr = importlib.import_module("dbs-gym_amd.hostrng")
+ms = importlib.import_module("dbs-gym_amd.model_setup")
+
+SEEDS = [0, 1, 7, 228, 12345, 2**31 - 1, 2**32 - 1, 10_000_007]
+
+
+def _same_state(a, b):
+    return a[0] == b[0] and np.array_equal(a[1], b[1]) and tuple(a[2:]) == tuple(b[2:])
+
+
+@pytest.mark.parametrize("seed", SEEDS)
+def test_stream_matches_randomstate(seed):
+    rs = np.random.RandomState(seed)
+    st = hr.StreamBank([seed]).stream(0)
+    seq = [("rand", (1000,), {}), ("uniform", (0.3, 0.8, 777), {}), ("normal", (np.pi, 0.6, 1001), {}),
+           ("randn", (3,), {}), ("normal", (1.0, 2.0, 2), {}), ("choice", ([1, 2, 3],), {}),
+           ("randn", (1,), {}), ("normal", (), {"loc": 0.5, "scale": 0.1, "size": (4, 5)}), ("rand", (), {}),
+           ("uniform", (), {}), ("randint", (0, 10, 7), {}), ("normal", (), {}), ("random_sample", (9,), {})]
+    for name, a, k in seq:
+        x, y = getattr(rs, name)(*a, **k), getattr(st, name)(*a, **k)
+        assert np.array_equal(np.asarray(x), np.asarray(y)), name
+        assert _same_state(rs.get_state(), st.get_state()), name
+
+
+def test_bank_draws_equal_per_stream_draws():
+    """The batch entry points (rows drawn in parallel) equal each stream drawn
+    alone, for a permuted row subset with per-row parameters."""
+    seeds = list(range(100, 164))
+    bank = hr.StreamBank(seeds)
+    rows = np.random.default_rng(0).permutation(64)[:40]
+    lo = np.linspace(-1, 1, 40)
+    hi = lo + np.linspace(0.5, 3, 40)
+    a = bank.random_sample(rows, 333)
+    b = bank.uniform(rows, lo, hi, 100)
+    c = bank.normal(rows, lo, hi - lo, 257)
+    for i, r in enumerate(rows):
+        rs = np.random.RandomState(seeds[r])
+        assert np.array_equal(a[i], rs.rand(333))
+        assert np.array_equal(b[i], rs.uniform(lo[i], hi[i], 100))
+        assert np.array_equal(c[i], rs.normal(lo[i], hi[i] - lo[i], 257))
+        assert _same_state(bank.get_state(int(r)), rs.get_state())
+    untouched = sorted(set(range(64)) - set(rows.tolist()))
+    for r in untouched:
+        assert _same_state(bank.get_state(r), np.random.RandomState(seeds[r]).get_state())
+
+
+@pytest.mark.parametrize("m", [1, 5, 8, 9, 127, 128, 129, 255, 1000, 1024, 4099, 8192, 8193, 10000, 16384, 20001])
+def test_remove_nonpositive_matches_reference_function(m):
+    """kh_remove_nonpositive == model_setup.remove_negative_w0 (utils.py:819-823)
+    on a RandomState: the same k draws, and numpy's pairwise-summed mean."""
+    gen = np.random.default_rng(m)
+    x = gen.normal(0.3, 1.0, (6, m))
+    x[0] = np.abs(x[0]) + 0.1        # a row with nothing to replace draws nothing
+    x[1, ::3] = 0.0                  # exact zeros count
+    seeds = [31 * m + i for i in range(6)]
+    bank = hr.StreamBank(seeds)
+    got = x.copy()
+    bank.remove_nonpositive(np.arange(6), got)
+    for i in range(6):
+        rs = np.random.RandomState(seeds[i])
+        want = ms.remove_negative_w0(rs, x[i].copy())
+        assert np.array_equal(got[i], want), i
+        assert _same_state(bank.get_state(i), rs.get_state()), i
+
+
+def test_state_round_trip_with_cached_gaussian():
+    rs = np.random.RandomState(5)
+    rs.normal(size=3)                       # odd count: a Gaussian is cached
+    assert rs.get_state()[3] == 1
+    bank = hr.StreamBank([0, 1])
+    bank.set_state(1, rs.get_state())
+    assert _same_state(bank.get_state(1), rs.get_state())
+    assert np.array_equal(bank.normal([1], 0.0, 1.0, 5)[0], rs.normal(0.0, 1.0, 5))
+    st = bank.stream(1)
+    st.seed(99)
+    assert _same_state(st.get_state(), np.random.RandomState(99).get_state())
+
+
+def test_interp_matches_the_w0_inverse_cdf():
+    ms.w0_from_uniform(np.zeros(1))
+    f = ms._INV_CDF
+    u = np.random.RandomState(3).rand(50_000)
+    u[:len(f.x)] = f.x                                        # table points exactly
+    u[-8:] = [0.0, 1e-300, f.x[0] * 0.5, f.x[-1], 1.0, 2.0, -1.0, f.x[len(f.x) // 2]]
+    got = hr.interp(u, f.x, f.y, f.fill_value[0], f.fill_value[1])
+    assert np.array_equal(got, f(u))
+    assert np.array_equal(ms.w0_from_uniform(u.reshape(50, 1000)), f(u).reshape(50, 1000))
+    assert np.isnan(hr.interp(np.array([np.nan]), f.x, f.y, 0.0, 1.0)[0])
+
+
+def test_argument_checks():
+    with pytest.raises(ValueError):
+        hr.StreamBank([-1])
+    with pytest.raises(ValueError):
+        hr.StreamBank([2**32])
+    bank = hr.StreamBank([1, 2])
+    with pytest.raises(ValueError, match="distinct"):
+        bank.random_sample([0, 0], 4)
+    with pytest.raises(ValueError):
+        bank.remove_nonpositive([0, 1], np.zeros((2, 4), np.float32))
+    with pytest.raises(ValueError):
+        bank.normal([0], 0.0, -1.0, 3)
+
+
+def test_envhost_streams_match_randomstate_hosts():
+    """A batch's hosts on one native bank draw what hosts on their own numpy
+    RandomState(rand_seed) draw, reset after reset (env2: drift events, whose
+    choice() draws go through the numpy fallback)."""
+    kura = importlib.import_module("dbs-gym_amd")
+    batch = importlib.import_module("dbs-gym_amd.batch")
+    base = kura.reference_params("env2")
+    plist = []
+    for b in range(6):
+        p = dict(base)
+        p["rand_seed"] = 40 + b
+        plist.append(p)
+    plist = kura.fill_driver_arrays_batch(plist, [900 + b for b in range(6)])
+    h_native, _ = kura.build_batch(plist)
+    assert all(isinstance(h.rs, hr.Stream) for h in h_native)
+    h_numpy = [batch.EnvHost(p, rs=np.random.RandomState()) for p in plist]
+    for _ in range(7):
+        a = batch.reset_draws_batch(h_native)
+        b = [h.reset_draws() for h in h_numpy]
+        for k in range(4):
+            assert np.array_equal(a[k], np.stack([r[k] for r in b])), k
+    for x, y in zip(h_native, h_numpy):
+        assert _same_state(x.rs.get_state(), y.rs.get_state())
