@@ -179,7 +179,7 @@ class EnvHost:
                repr(list(p["grid_size"])), bool(p["naive_dbs"]), bool(p.get("directed_stimulation")))
         if getattr(self, "_g_key", None) != key:
             # shared by the envs of a process that sit on the same grid with the same contacts
-            ck = (self.grid.tobytes(),) + key
+            ck = (_grid_key(self.grid),) + key
             hit = _COND_CACHE.get(ck)
             if hit is None:
                 gs, naive = p["grid_size"], p["naive_dbs"]
@@ -198,6 +198,22 @@ class EnvHost:
 
 
 _COND_CACHE: dict = {}   # (grid bytes, contacts, modifier, settings) -> read-only (g_stim, g_rec)
+_GRID_KEYS: dict = {}    # id(read-only grid) -> (grid, its bytes): one bytes object (hashed once) per grid
+
+
+def _grid_key(grid: np.ndarray) -> bytes:
+    """grid.tobytes(), shared by every env on the same read-only grid array
+    (fill_driver_arrays_batch hands all envs of a geometry the same one), so
+    the 24 KB key is built and hashed once, not once per env."""
+    if grid.flags.writeable:
+        return grid.tobytes()
+    e = _GRID_KEYS.get(id(grid))
+    if e is None or e[0] is not grid:
+        if len(_GRID_KEYS) >= 64:
+            _GRID_KEYS.clear()
+        e = (grid, grid.tobytes())
+        _GRID_KEYS[id(grid)] = e
+    return e[1]
 
 
 def _check_w0(w0: np.ndarray) -> None:
@@ -218,7 +234,12 @@ def reset_draws_batch(hosts: list[EnvHost]):
       env.py:595-598  theta0 = normal(mean, sd, N) per env, then
                       remove_negative_w0(theta0) (again only when needed).
     Returns (w0 (n, N), g_stim (n, ne, N), g_rec (n, nr, N), theta0 (n, N)),
-    float64; each host keeps its w0 (a row of the returned array)."""
+    float64; each host keeps its w0 (a row of the returned array).
+    Hosts that are not EnvHosts (evaluation.ReplayHost: pre-drawn resets)
+    answer their own reset_draws()."""
+    if not all(isinstance(h, EnvHost) for h in hosts):
+        d = [h.reset_draws() for h in hosts]
+        return tuple(np.stack([np.asarray(r[k], np.float64) for r in d]) for k in range(4))
     for h in hosts:
         h._advance_events()
     w0wo = np.stack([h.w0_without_locus for h in hosts])

@@ -1109,8 +1109,19 @@ __device__ __forceinline__ void save_pass(const DevParams& __restrict__ p, const
     int fin = 0;  // wave-uniform: rounds holding some env's final row (bit k)
 #pragma unroll
     for (int k = 0; k < RCX; ++k) fin |= __any((flor >> (3 * k)) & 4) ? (1 << k) : 0;
-    float* const yout = p.y;
-    float* const rows = p.rows;
+    // final state and captured rows: raw buffer stores through descriptors
+    // over this env group's valid envs, one unconditional store per element;
+    // an element that is not stored gets an offset past the range, which the
+    // hardware drops.  (Per-element exec-masked flat stores here lost almost
+    // every final-state store of the split kernel with parts of 512 in some
+    // builds -- the sums of the same pass were right -- DESIGN.md section 5.)
+    const int nvalid = Bn - env_base < E_WG ? Bn - env_base : E_WG;
+    const __amdgpu_buffer_rsrc_t ys = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)uniform_ptr(p.y + (size_t)env_base * NG), 0, nvalid * NG * 4, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rws = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)uniform_ptr(p.rows ? p.rows + (size_t)env_base * (KURA_S_MAX + 1) * NG : p.y), 0,
+        p.rows ? nvalid * (KURA_S_MAX + 1) * NG * 4 : 0, 0x00020000);
+    constexpr int kDrop = 0x7ffffff0;   // past every range: the store is dropped
     int rbase[8];  // captured row index of round 0 of this pass: sol_state_ row si - lfp_from + pos0
     if (capture) {
 #pragma unroll
@@ -1191,17 +1202,18 @@ __device__ __forceinline__ void save_pass(const DevParams& __restrict__ p, const
 #pragma unroll
                         for (int qq = 0; qq < 4; ++qq) {
                             const int q = 4 * hh + qq;
-                            const int env = env_base + mfma_env(q, lane);
-                            if (((fl[q] >> (3 * k)) & 4) && env < Bn) yout[(size_t)env * NG + col0 + i] = v[qq];
+                            const int off = (mfma_env(q, lane) * NG + col0 + i) * 4;
+                            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[qq]), ys,
+                                                                  ((fl[q] >> (3 * k)) & 4) ? off : kDrop, 0, 0);
                         }
                     }
                     if (capture) {
 #pragma unroll
                         for (int qq = 0; qq < 4; ++qq) {
                             const int q = 4 * hh + qq;
-                            const int env = env_base + mfma_env(q, lane);
-                            if (((fl[q] >> (3 * k)) & 1) && env < Bn)
-                                rows[((size_t)env * (KURA_S_MAX + 1) + rbase[q] + k) * NG + col0 + i] = v[qq];
+                            const int off = ((mfma_env(q, lane) * (KURA_S_MAX + 1) + rbase[q] + k) * NG + col0 + i) * 4;
+                            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[qq]), rws,
+                                                                  ((fl[q] >> (3 * k)) & 1) ? off : kDrop, 0, 0);
                         }
                     }
                 }
@@ -1258,16 +1270,17 @@ __device__ __forceinline__ void save_pass(const DevParams& __restrict__ p, const
             if ((fin >> k) & 1) {  // the solve's last row: the new state
 #pragma unroll
                 for (int q = 0; q < 8; ++q) {
-                    const int env = env_base + mfma_env(q, lane);
-                    if (((fl[q] >> (3 * k)) & 4) && env < Bn) yout[(size_t)env * NG + col0 + i] = v[q];
+                    const int off = (mfma_env(q, lane) * NG + col0 + i) * 4;
+                    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[q]), ys,
+                                                          ((fl[q] >> (3 * k)) & 4) ? off : kDrop, 0, 0);
                 }
             }
             if (capture) {
 #pragma unroll
                 for (int q = 0; q < 8; ++q) {
-                    const int env = env_base + mfma_env(q, lane);
-                    if (((fl[q] >> (3 * k)) & 1) && env < Bn)
-                        rows[((size_t)env * (KURA_S_MAX + 1) + rbase[q] + k) * NG + col0 + i] = v[q];
+                    const int off = ((mfma_env(q, lane) * (KURA_S_MAX + 1) + rbase[q] + k) * NG + col0 + i) * 4;
+                    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[q]), rws,
+                                                          ((fl[q] >> (3 * k)) & 1) ? off : kDrop, 0, 0);
                 }
             }
         }

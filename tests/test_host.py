@@ -133,3 +133,18 @@ def test_batched_driver_fill_and_reset_draws_are_bit_identical():
     for a, b in zip(h1, h2):
         sa, sb = a.rs.get_state(), b.rs.get_state()
         assert np.array_equal(sa[1], sb[1]) and sa[2:] == sb[2:]
+
+
+def test_reset_draws_batch_replay_hosts():
+    """evaluation.ReplayHost (pre-drawn resets of the eval protocol) goes
+    through reset_draws_batch like an EnvHost: its own draws, stacked."""
+    ev = importlib.import_module("dbs-gym_amd.evaluation")
+    batch = importlib.import_module("dbs-gym_amd.batch")
+    rng = np.random.default_rng(1)
+    d = [[(rng.random(8), rng.random((2, 8)), rng.random((1, 8)), rng.random(8)) for _ in range(2)] for _ in range(3)]
+    hosts = [ev.ReplayHost(x) for x in d]
+    for r in range(2):
+        w0, gs, gr, th = batch.reset_draws_batch(hosts)
+        for k, x in enumerate(d):
+            for got, want in zip((w0[k], gs[k], gr[k], th[k]), x[r]):
+                np.testing.assert_array_equal(got, want)
