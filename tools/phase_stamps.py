@@ -73,7 +73,7 @@ def main():
     nwg = (cfg.n_envs + 15) // 16
     cyc_per_step_wave = s.sum(axis=0) / (nwaves * nwg * nsteps)
     out = {"mode": os.environ.get("MODE", "step"), "ms_per_launch": ev_ms,
-           "kernel": KERN, "share": dict(zip(names, [round(float(x), 4) for x in share])),
+           "kernel": "K1", "share": dict(zip(names, [round(float(x), 4) for x in share])),
            "cycles_per_step_per_wave": dict(zip(names, [round(float(x)) for x in cyc_per_step_wave])),
            # per wave (rows), cycles per step of the phases that differ between waves
            "per_wave": {names[k]: [round(float(v)) for v in s[:, k] / (nwg * nsteps)]
