@@ -61,7 +61,7 @@ class EnvHost:
     constructs several envs in one process (it is reseeded here with this
     env's rand_seed, as SpatialKuramoto.__init__ does, env.py:291)."""
 
-    def __init__(self, params: dict, rs=None, stream=None):
+    def __init__(self, params: dict, rs=None, stream=None, defer_perturbations: bool = False):
         p = params
         self.p = p
         if rs is not None:
@@ -105,9 +105,11 @@ class EnvHost:
             self.plasticity_percent = p["plasticity_percent"]
             self.reset_plasticity_episode = p["reset_plasticity_episode"]
             self.plasticity_process_count = 0
-            self.w0_process = ms.generate_perturbations(self.rs, self.w0_without_locus,
-                                                        M=self.reset_plasticity_episode * 2,
-                                                        step_scale=self.plasticity_percent * 0.01)
+            self.w0_process = None
+            if not defer_perturbations:     # else the caller draws it (perturb_batch), first on this stream
+                self.w0_process = ms.generate_perturbations(self.rs, self.w0_without_locus,
+                                                            M=self.reset_plasticity_episode * 2,
+                                                            step_scale=self.plasticity_percent * 0.01)
         self.spatial_events = []
         self.spatial_var_freq = p["spatial_var_freq"]                          # env.py:382-384
         self.spatial_var_episode = self.spatial_var_freq
@@ -128,6 +130,15 @@ class EnvHost:
     def _advance_events(self):
         """env.py:473-557: the reset counter and the drift / spatial-variation
         events of this reset (their draws, in the reference's order)."""
+        if self._advance_drift():
+            perturb_batch([self])
+        self._advance_spatial()
+
+    def _advance_drift(self) -> bool:
+        """env.py:473-531 and the first half of :532-541: the reset counter and
+        the temporal-drift events; returns whether this reset regenerates the
+        plasticity random walk (env.py:535-541), which the caller then draws
+        (perturb_batch) before _advance_spatial."""
         p = self.p
         self.reset_count += 1
         if p["temporal_drift"]:
@@ -154,9 +165,12 @@ class EnvHost:
             if self.reset_count % self.reset_plasticity_episode == 0:           # env.py:532-541
                 self.plasticity_process_count = 0
                 self.w0_without_locus = deepcopy(self.w0_without_locus_)
-                self.w0_process = ms.generate_perturbations(self.rs, self.w0_without_locus,
-                                                            M=self.reset_plasticity_episode * 2,
-                                                            step_scale=self.plasticity_percent * 0.01)
+                return True
+        return False
+
+    def _advance_spatial(self):
+        """env.py:544-557: the spatial-variation event of this reset."""
+        p = self.p
         if p["spatial_feature"]:                                               # env.py:544-557
             if self.spatial_var_episode == self.reset_count and self.reset_count > 2:
                 index = self.rs.choice(len(STIM_REC_LOCUS))
@@ -216,6 +230,25 @@ def _grid_key(grid: np.ndarray) -> bytes:
     return e[1]
 
 
+def perturb_batch(hosts: list[EnvHost]) -> None:
+    """host.w0_process = generate_perturbations(host.rs, host.w0_without_locus,
+    M=2*reset_plasticity_episode, step_scale=plasticity_percent/100)
+    (env.py:21-57, :377, :537-541) for each host: one native call per stream
+    bank and (M, step) for hosts on native streams, numpy otherwise (in list
+    order, for a shared RandomState)."""
+    groups: dict = {}
+    for h in hosts:
+        M, step = h.reset_plasticity_episode * 2, h.plasticity_percent * 0.01
+        if isinstance(h.rs, hostrng.Stream):
+            groups.setdefault((id(h.rs.bank), M, step), (h.rs.bank, []))[1].append(h)
+        else:
+            h.w0_process = ms.generate_perturbations(h.rs, h.w0_without_locus, M=M, step_scale=step)
+    for (_b, M, step), (bank, hs) in groups.items():
+        out = bank.perturbations([h.rs.row for h in hs], np.stack([h.w0_without_locus for h in hs]), M, step)
+        for h, o in zip(hs, out):
+            h.w0_process = o
+
+
 def _check_w0(w0: np.ndarray) -> None:
     if np.min(w0) < 0:
         raise AssertionError("Natural frequencies w0 must be positive!")       # env.py:214
@@ -240,8 +273,10 @@ def reset_draws_batch(hosts: list[EnvHost]):
     if not all(isinstance(h, EnvHost) for h in hosts):
         d = [h.reset_draws() for h in hosts]
         return tuple(np.stack([np.asarray(r[k], np.float64) for r in d]) for k in range(4))
+    regen = [h for h in hosts if h._advance_drift()]   # each env's draws stay in the reference's order:
+    perturb_batch(regen)                                 # drift events, the plasticity walk, spatial events
     for h in hosts:
-        h._advance_events()
+        h._advance_spatial()
     w0wo = np.stack([h.w0_without_locus for h in hosts])
     wl = np.stack([np.asarray(h.p["locus_without_w0"], np.float64) for h in hosts])
     lm0 = hosts[0].p["locus_mask"] if hosts else None
@@ -384,8 +419,9 @@ def build_batch(params_list: list[dict]) -> tuple[list[EnvHost], dict]:
           for p in params_list]
     rows = np.cumsum(ok) - 1
     bank = hostrng.StreamBank([int(p["rand_seed"]) for p, o in zip(params_list, ok) if o])
-    hosts = [EnvHost(p, stream=bank.stream(int(r)) if o else None)
+    hosts = [EnvHost(p, stream=bank.stream(int(r)) if o else None, defer_perturbations=bool(o))
              for p, o, r in zip(params_list, ok, rows)]
+    perturb_batch([h for h in hosts if getattr(h, "w0_process", 0) is None])   # env.py:377, on each env's own stream
     p0 = params_list[0]
     for p in params_list[1:]:
         if p["num_oscillators"] != p0["num_oscillators"] or list(p["grid_size"]) != list(p0["grid_size"]):

@@ -240,3 +240,40 @@ void kh_interp(const double* x, int64_t n, const double* xp, const double* fp, i
         out[i] = r;
     }
 }
+
+// numpy's float64 add.reduce of a contiguous vector (the inner loop over
+// buffers of 8192 elements, each a pairwise sum), from 0.0
+static double kh_reduce_sum(const double* a, int64_t n) {
+    double sum = 0.0;
+    for (int64_t c = 0; c < n; c += 8192) sum += kh_pairwise_sum(a + c, n - c < 8192 ? n - c : 8192);
+    return sum;
+}
+
+// generate_perturbations (environment/env.py:21-57) of row i of initial
+// (n rows of m) with stream rows[i]: out[i] (M+1 rows of m) = the random walk
+// initial, initial + s*g_1, ... with s = step_scale * std(initial, ddof=1)
+// (numpy's std: pairwise mean, squared deviations, pairwise sum / (m-1),
+// sqrt) and g_k = randn(m).  tmp: n*m doubles of scratch.
+void kh_perturbations(kh_mt* streams, const int64_t* rows, int64_t n, const double* initial, int64_t m, int64_t M,
+                      double step_scale, double* out, double* tmp) {
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < n; ++i) {
+        kh_mt* s = &streams[rows[i]];
+        const double* x = initial + i * m;
+        double* o = out + i * (M + 1) * m;
+        double* d = tmp + i * m;
+        const double mean = kh_reduce_sum(x, m) / (double)m;
+        for (int64_t j = 0; j < m; ++j) {
+            const double v = x[j] - mean;
+            d[j] = v * v;
+        }
+        const double var = kh_reduce_sum(d, m) / (double)(m - 1);
+        const double sc = step_scale * sqrt(var);
+        for (int64_t j = 0; j < m; ++j) o[j] = x[j];
+        for (int64_t k = 1; k <= M; ++k) {
+            const double* cur = o + (k - 1) * m;
+            double* nxt = o + k * m;
+            for (int64_t j = 0; j < m; ++j) nxt[j] = cur[j] + sc * kh_gauss1(s);
+        }
+    }
+}

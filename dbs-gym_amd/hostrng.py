@@ -41,6 +41,7 @@ def lib():
                            ("kh_normal", [P, P, I64, P, P, I64, P]),
                            ("kh_randn", [P, I64, I64, P]),
                            ("kh_remove_nonpositive", [P, P, I64, P, I64]),
+                           ("kh_perturbations", [P, P, I64, P, I64, I64, D, P, P]),
                            ("kh_interp", [P, I64, P, P, I64, D, D, P])):
             f = getattr(L, name)
             f.restype = None
@@ -124,6 +125,20 @@ class StreamBank:
         if x.dtype != np.float64 or not x.flags.c_contiguous or x.ndim != 2 or x.shape[0] != len(rows):
             raise ValueError("remove_nonpositive: x must be C-contiguous float64 of shape (len(rows), m)")
         lib().kh_remove_nonpositive(_ptr(self.state), _ptr(rows), len(rows), _ptr(x), x.shape[1])
+
+    def perturbations(self, rows, initial: np.ndarray, M: int, step_scale: float) -> np.ndarray:
+        """model_setup.generate_perturbations (env.py:21-57) for each row of
+        initial (len(rows), m), row i drawing from stream rows[i]:
+        (len(rows), M + 1, m) float64."""
+        rows = _rows(rows)
+        x = np.ascontiguousarray(initial, dtype=np.float64)
+        if x.ndim != 2 or x.shape[0] != len(rows) or x.shape[1] < 2:
+            raise ValueError("perturbations: initial must be (len(rows), m >= 2)")
+        out = np.empty((len(rows), int(M) + 1, x.shape[1]))
+        tmp = np.empty_like(x)
+        lib().kh_perturbations(_ptr(self.state), _ptr(rows), len(rows), _ptr(x), x.shape[1], int(M),
+                               float(step_scale), _ptr(out), _ptr(tmp))
+        return out
 
     def randn(self, row: int, m: int) -> np.ndarray:
         out = np.empty(int(m))

@@ -135,3 +135,17 @@ def test_envhost_streams_match_randomstate_hosts():
             assert np.array_equal(a[k], np.stack([r[k] for r in b])), k
     for x, y in zip(h_native, h_numpy):
         assert _same_state(x.rs.get_state(), y.rs.get_state())
+
+
+@pytest.mark.parametrize("m", [2, 7, 1024, 9000])
+def test_perturbations_match_generate_perturbations(m):
+    """kh_perturbations == model_setup.generate_perturbations (env.py:21-57) on
+    a RandomState: numpy's std(ddof=1), the walk, the stream position."""
+    init = np.random.default_rng(m).normal(3.0, 1.0, (5, m))
+    bank = hr.StreamBank([11 + i for i in range(5)])
+    got = bank.perturbations(np.arange(5), init, 20, 0.05)
+    for i in range(5):
+        rs = np.random.RandomState(11 + i)
+        want = ms.generate_perturbations(rs, init[i], M=20, step_scale=0.05)
+        assert np.array_equal(got[i], want)
+        assert _same_state(bank.get_state(i), rs.get_state())
