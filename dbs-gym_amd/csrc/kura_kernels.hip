@@ -110,6 +110,18 @@ struct DevParams {
     float* rows;            // optional [B][KURA_S_MAX+1][N]: every saved row of a step (sol_state_, env.py:430,440)
 };
 
+// Device code reads DevParams where the dispatch put it: in the kernarg
+// segment (constant address space, scalar loads).  Every kernel takes it by
+// value as its FIRST argument (so it sits at kernarg offset 0) and reads it
+// through kargs(); taking the by-value parameter's address instead makes the
+// compiler copy the ~600-byte struct into every lane's scratch for the
+// called solver to point at (K1 <4, false>: 1152 -> 560 B of scratch per
+// lane, profiles/r04_resource_usage.txt; +0.8 % in the same-box A/B).
+typedef const __attribute__((address_space(4))) DevParams DevParamsK;
+__device__ __forceinline__ DevParamsK& kargs() {
+    return *(DevParamsK*)__builtin_amdgcn_kernarg_segment_ptr();
+}
+
 // Diagnostic phase timers (compile with -DKURA_STAMPS): per wave, cycles
 // spent in each phase (tools/phase_stamps.py names them), accumulated with
 // s_memtime and added into p.stamps[wave][KURA_NSTAMP] at the end.
@@ -517,7 +529,7 @@ struct Slot {
     }
 };
 // the records of workgroup pair `pair`, this wave's tiles from ct0
-__device__ __forceinline__ Slot make_slot(const DevParams& p, int pair, int N, int ct0) {
+__device__ __forceinline__ Slot make_slot(DevParamsK& p, int pair, int N, int ct0) {
     const int lane = threadIdx.x & 63;
     Slot s{__builtin_amdgcn_make_buffer_rsrc((void*)uniform_ptr(p.R + (size_t)pair * NSLOT * N * 16), 0,
                                              NSLOT * N * 16 * 4, 0x00020000),
@@ -581,7 +593,7 @@ __device__ __forceinline__ void store8(const Slot& w, int slot, int t, const flo
 // start of the solve; all TPW tiles' loads are issued before the first use)
 // (split groups read this part's sin/cos from its published global image)
 template <int TPW, bool XL>
-__device__ __forceinline__ void coupling_epilogue(const DevParams& __restrict__ p, const Slot& ws, const float* __restrict__ Xs,
+__device__ __forceinline__ void coupling_epilogue(DevParamsK& __restrict__ p, const Slot& ws, const float* __restrict__ Xs,
                                                   const float* __restrict__ xown, const floatx16 (&acc)[TPW],
                                                   int stage, bool pulse_on) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -836,7 +848,8 @@ __device__ __forceinline__ void store_sc1_x4(float* dst, const floatx4& v) {
 // completes (a part not resident) gives up after ~1 s and raises stats flag
 // bit 4 (every later barrier of the launch then gives up at once) instead of
 // hanging the GPU.
-__device__ __noinline__ void group_barrier(const DevParams& p, Part& pt) {
+__device__ __noinline__ void group_barrier(DevParamsK& pin, Part& pt) {
+    DevParamsK& p = *uniform_ptr(&pin);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     pt.ep += 1;
@@ -866,7 +879,7 @@ __device__ __noinline__ void group_barrier(const DevParams& p, Part& pt) {
 // part's values v[k] (k < nk); on return it holds 0 + part_0 + part_1 + ...
 // (part order) -- the RM order extended over parts (oracle_rm_*).
 template <int NK>
-__device__ __forceinline__ void group_sum(const DevParams& p, Part& pt, float (&vf)[NK], double (&vd)[NK], int nk,
+__device__ __forceinline__ void group_sum(DevParamsK& p, Part& pt, float (&vf)[NK], double (&vd)[NK], int nk,
                                           bool with_d) {
     const int tid = threadIdx.x;
     const int grp = __builtin_amdgcn_readfirstlane(pt.group), npart = __builtin_amdgcn_readfirstlane(pt.npart);
@@ -901,7 +914,7 @@ __device__ __forceinline__ void group_sum(const DevParams& p, Part& pt, float (&
 // Publish this part's sin/cos image (LDS, xl_img(TPW) floats) into the group's
 // image buffer and wait until every part has published its own.
 template <int TPW>
-__device__ __forceinline__ const float* group_publish_x(const DevParams& p, Part& pt, const float* Xs) {
+__device__ __forceinline__ const float* group_publish_x(DevParamsK& p, Part& pt, const float* Xs) {
     constexpr int XL_IMG = xl_img(TPW);
     const int grp = __builtin_amdgcn_readfirstlane(pt.group), npart = __builtin_amdgcn_readfirstlane(pt.npart);
     const size_t img = ((size_t)grp * 2 + (__builtin_amdgcn_readfirstlane(pt.xs_n) & 1)) * npart * XL_IMG;
@@ -963,7 +976,7 @@ __device__ __forceinline__ void err_dense_tile(const DP& p, const Slot& ws, int 
 // per Dopri step).  Same operations, same order as the two passes; measured
 // 2 % slower than the separate passes, so not the default.
 template <int TPW, bool XL>
-__device__ __forceinline__ void coupling_epilogue_err(const DevParams& __restrict__ p, const Slot& ws,
+__device__ __forceinline__ void coupling_epilogue_err(DevParamsK& __restrict__ p, const Slot& ws,
                                                       const float* __restrict__ Xs, const float* __restrict__ xown,
                                                       const floatx16 (&acc)[TPW], bool pulse_on) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -1042,7 +1055,7 @@ __device__ __forceinline__ void save_rounds_setup(const CtlE& c, int e, int r0) 
 }
 
 template <int TPW, bool XL, int RCX>
-__device__ __forceinline__ void save_pass(const DevParams& __restrict__ p, const Slot& ws, int env_base, bool to_ring, Part& pt,
+__device__ __forceinline__ void save_pass(DevParamsK& __restrict__ p, const Slot& ws, int env_base, bool to_ring, Part& pt,
                                           const float (&h)[8], int r0, int nrounds, bool gauss STAMP_PARAMS) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, tid = threadIdx.x;
     const int NG = XL ? __builtin_amdgcn_readfirstlane(pt.ng) : TPW * 256;
@@ -1353,7 +1366,7 @@ __device__ __forceinline__ void save_pass(const DevParams& __restrict__ p, const
 
 // Returns whether any env of the workgroup goes on integrating (uniform).
 template <int TPW, bool XL>
-__device__ __forceinline__ int post_step(const DevParams& __restrict__ p, Slot& ws, int env_base, bool to_ring, Part& pt
+__device__ __forceinline__ int post_step(DevParamsK& __restrict__ p, Slot& ws, int env_base, bool to_ring, Part& pt
                                          STAMP_PARAMS) {
     const int lane = threadIdx.x & 63, tid = threadIdx.x;
     const int NG = XL ? __builtin_amdgcn_readfirstlane(pt.ng) : TPW * 256;   // oscillators per env
@@ -1521,8 +1534,13 @@ __device__ __forceinline__ int post_step(const DevParams& __restrict__ p, Slot& 
 #define KURA_SOLVE_ATTR __noinline__
 #endif
 template <int TPW, bool XL>
-__device__ KURA_SOLVE_ATTR void solve_wg(const DevParams& __restrict__ p, float* Xs, int env_base, bool to_ring, bool pulse_on,
+__device__ KURA_SOLVE_ATTR void solve_wg(DevParamsK& __restrict__ pin, float* Xs, int env_base, bool to_ring, bool pulse_on,
                          long long* rhs_count, Part& pt) {
+    // (the kernarg segment through the VGPR-passed pointer: vector loads.
+    // Made wave-uniform -- scalar loads, which share lgkmcnt with the LDS
+    // traffic -- the step was 1.5 % slower in the same-box A/B,
+    // profiles/r04_kargs_ab.txt)
+    DevParamsK& __restrict__ p = pin;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, tid = threadIdx.x;
     constexpr int N = TPW * 256;            // oscillators owned by this workgroup
     const int NG = XL ? __builtin_amdgcn_readfirstlane(pt.ng) : N;      // oscillators per env
@@ -1615,7 +1633,7 @@ __device__ KURA_SOLVE_ATTR void solve_wg(const DevParams& __restrict__ p, float*
     *rhs_count += nrhs;
 }
 
-__device__ __forceinline__ void flush_stats(const DevParams& p, long long rhs, int env_base) {
+__device__ __forceinline__ void flush_stats(DevParamsK& p, long long rhs, int env_base) {
     if (threadIdx.x != 0) return;
     unsigned long long steps = 0, rej = 0, flags = 0;
     for (int e = 0; e < E_WG; ++e) {
@@ -1685,7 +1703,7 @@ struct WinView {
 //   R2:      d = c . x, the filtfilt term as a linear functional (kura_r2.h:
 //            f[-1] - mean(f) of scipy's filtfilt is linear in the window).
 template <int WPL>
-__device__ __forceinline__ double reward_of(const DevParams& p, const double (&x)[WPL], double u0) {
+__device__ __forceinline__ double reward_of(DevParamsK& p, const double (&x)[WPL], double u0) {
     const double au = fabs(u0);
     if (p.reward_kind == KURA_R_TEMP_CONST) {
         const double d = window_dot<WPL>(x, p.r2c, p.W);
@@ -1719,7 +1737,7 @@ __device__ __forceinline__ double reward_of(const DevParams& p, const double (&x
 // wave-uniform descriptor), the windows straight from the ring / this step's
 // samples (WinView).  ok[e] false: d[e] = 0 and nothing of env e is read.
 template <int NE>
-__device__ __forceinline__ void r2_dot_multi(const DevParams& __restrict__ p, const WinView (&xv)[NE],
+__device__ __forceinline__ void r2_dot_multi(DevParamsK& __restrict__ p, const WinView (&xv)[NE],
                                              const bool (&ok)[NE], double (&d)[NE]) {
     const int lane = threadIdx.x & 63;
     const int W = p.W;
@@ -1761,7 +1779,7 @@ __device__ __forceinline__ void r2_dot_multi(const DevParams& __restrict__ p, co
 // episode, tests/test_oracle_props.py).
 
 // whole wave: Y of env `env` from its ring (positions 0..W-1), R64 dots
-__device__ __forceinline__ void spec_init(const DevParams& __restrict__ p, int env) {
+__device__ __forceinline__ void spec_init(DevParamsK& __restrict__ p, int env) {
     const int lane = threadIdx.x & 63;
     const int W = p.W, nb = p.n_bins;
     const double* rb = p.ring + (size_t)env * W;
@@ -1787,7 +1805,7 @@ __device__ __forceinline__ void spec_init(const DevParams& __restrict__ p, int e
 // band power of the new window (the bins summed in index order from +0, as
 // calc_beta_band_power's np.sum does in the oracle).  Lane j < 2 n_bins owns
 // Y's component j (bin j/2, re or im) and walks the S slots in order.
-__device__ __forceinline__ double spec_step(const DevParams& __restrict__ p, int e, int env, int wp0, int S) {
+__device__ __forceinline__ double spec_step(DevParamsK& __restrict__ p, int e, int env, int wp0, int S) {
     const int lane = threadIdx.x & 63;
     const int W = p.W, nb = p.n_bins;
     // the values the S appends overwrite, read before any of them is stored
@@ -1821,7 +1839,7 @@ __device__ __forceinline__ double spec_step(const DevParams& __restrict__ p, int
 
 // reward_of's closing expressions (env.py:638-688) from the band power bb (R1,
 // R3) or the filter term d (R2)
-__device__ __forceinline__ double reward_from(const DevParams& p, double bb, double d, double u0) {
+__device__ __forceinline__ double reward_from(DevParamsK& p, double bb, double d, double u0) {
     const double au = fabs(u0);
     if (p.reward_kind == KURA_R_TEMP_CONST) {
         const double r1 = 1e3 * (d * d);
@@ -1841,7 +1859,7 @@ __device__ __forceinline__ double reward_from(const DevParams& p, double bb, dou
 // group; split groups loop persistently over pairs with a grid that is a
 // multiple of npart and at most one workgroup per CU, so every part of a
 // group is resident at the same time.
-__device__ __forceinline__ Part make_part(const DevParams& p, int pair) {
+__device__ __forceinline__ Part make_part(DevParamsK& p, int pair) {
     Part pt;
     pt.npart = p.npart;
     pt.group = pair / p.npart;
@@ -1856,7 +1874,7 @@ __device__ __forceinline__ Part make_part(const DevParams& p, int pair) {
 
 // Launch-wide failure bits an env inherits: a split-group barrier that timed
 // out (group_barrier) leaves every later exchange of the launch unsynchronised.
-__device__ __forceinline__ int launch_flags(const DevParams& p, bool xl) {
+__device__ __forceinline__ int launch_flags(DevParamsK& p, bool xl) {
     if (!xl) return 0;  // split groups only: their group barriers can time out
     const unsigned long long v = __hip_atomic_load((__attribute__((address_space(1))) unsigned long long*)&p.stats[3],
                                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1864,7 +1882,7 @@ __device__ __forceinline__ int launch_flags(const DevParams& p, bool xl) {
 }
 
 template <int TPW, bool XL>
-__device__ __forceinline__ void step_pair(const DevParams& p, Part& pt, float* Xs, const float* __restrict__ action,
+__device__ __forceinline__ void step_pair(DevParamsK& p, Part& pt, float* Xs, const float* __restrict__ action,
                                           float* __restrict__ obs, double* __restrict__ reward,
                                           uint8_t* __restrict__ done, float* __restrict__ lfp_true,
                                           double* __restrict__ lfp_rec, int* __restrict__ nsamp) {
@@ -2037,18 +2055,20 @@ __device__ __forceinline__ void step_pair(const DevParams& p, Part& pt, float* X
 // -O2 as well (tools/parity_probe.py, profiles/r02_part256_probe.txt); the
 // GPU parity suite covers every instantiation.
 template <int TPW, bool XL>
-__device__ __noinline__ void step_pair_call(const DevParams& p, Part& pt, float* Xs, const float* __restrict__ action,
+__device__ __noinline__ void step_pair_call(DevParamsK& pin, Part& pt, float* Xs, const float* __restrict__ action,
                                             float* __restrict__ obs, double* __restrict__ reward,
                                             uint8_t* __restrict__ done, float* __restrict__ lfp_true,
                                             double* __restrict__ lfp_rec, int* __restrict__ nsamp) {
-    step_pair<TPW, XL>(p, pt, Xs, action, obs, reward, done, lfp_true, lfp_rec, nsamp);
+    step_pair<TPW, XL>(pin, pt, Xs, action, obs, reward, done, lfp_true, lfp_rec, nsamp);
 }
 
 template <int TPW, bool XL>
-__global__ __launch_bounds__(NTHREADS) void kura_step_kernel(DevParams p, const float* __restrict__ action,
+__global__ __launch_bounds__(NTHREADS) void kura_step_kernel(DevParams p_kernarg, const float* __restrict__ action,
                                                              float* __restrict__ obs, double* __restrict__ reward,
                                                              uint8_t* __restrict__ done, float* __restrict__ lfp_true,
                                                              double* __restrict__ lfp_rec, int* __restrict__ nsamp) {
+    DevParamsK& p = kargs();  // == p_kernarg, read in place (kernarg offset 0)
+    (void)p_kernarg;
     extern __shared__ float Xs[];  // xs_floats(min(N, 1024))
     if constexpr (XL) {
 #pragma unroll 1
@@ -2064,7 +2084,7 @@ __global__ __launch_bounds__(NTHREADS) void kura_step_kernel(DevParams p, const 
 
 // ----------------------------------------------------------- reset kernel --
 template <int TPW, bool XL>
-__device__ __forceinline__ void reset_pair(const DevParams& p, Part& pt, float* Xs, const uint8_t* __restrict__ mask,
+__device__ __forceinline__ void reset_pair(DevParamsK& p, Part& pt, float* Xs, const uint8_t* __restrict__ mask,
                                            const float* __restrict__ theta0, float* __restrict__ obs) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, tid = threadIdx.x;
     const int N = p.N, W = p.W;
@@ -2112,14 +2132,18 @@ __device__ __forceinline__ void reset_pair(const DevParams& p, Part& pt, float* 
 
 // kura_set_state / kura_set_spec(NULL) / kura_set_spectral: re-form every
 // env's spectral accumulators from its ring (one wave per env)
-__global__ __launch_bounds__(64) void kura_spec_init_kernel(DevParams p) {
+__global__ __launch_bounds__(64) void kura_spec_init_kernel(DevParams p_kernarg) {
+    DevParamsK& p = kargs();  // == p_kernarg, read in place (kernarg offset 0)
+    (void)p_kernarg;
     if ((int)blockIdx.x < p.B) spec_init(p, blockIdx.x);
 }
 
 template <int TPW, bool XL>
-__global__ __launch_bounds__(NTHREADS) void kura_reset_kernel(DevParams p, const uint8_t* __restrict__ mask,
+__global__ __launch_bounds__(NTHREADS) void kura_reset_kernel(DevParams p_kernarg, const uint8_t* __restrict__ mask,
                                                               const float* __restrict__ theta0,
                                                               float* __restrict__ obs) {
+    DevParamsK& p = kargs();  // == p_kernarg, read in place (kernarg offset 0)
+    (void)p_kernarg;
     extern __shared__ float Xs[];
     if constexpr (XL) {
 #pragma unroll 1
@@ -2135,9 +2159,11 @@ __global__ __launch_bounds__(NTHREADS) void kura_reset_kernel(DevParams p, const
 
 // ------------------------------------------------------ standalone reward --
 template <int WPL>
-__global__ __launch_bounds__(64) void kura_reward_kernel(DevParams p, const double* __restrict__ win,
+__global__ __launch_bounds__(64) void kura_reward_kernel(DevParams p_kernarg, const double* __restrict__ win,
                                                          const float* __restrict__ u0, double* __restrict__ out,
                                                          int n) {
+    DevParamsK& p = kargs();  // == p_kernarg, read in place (kernarg offset 0)
+    (void)p_kernarg;
     const int env = blockIdx.x;
     if (env >= n) return;
     const int lane = threadIdx.x;
@@ -2160,11 +2186,13 @@ __global__ __launch_bounds__(64) void kura_reward_kernel(DevParams p, const doub
 // host twiddle rows of length L (the same R64 order as window_dot, so a
 // length-W call equals kura_reward bit for bit), R2 = the R64 dot with the
 // length-L functional c (kura_r2.h; the host caches one per length).
-__global__ __launch_bounds__(64) void kura_reward_n_kernel(DevParams p, const double* __restrict__ x, long long ld,
+__global__ __launch_bounds__(64) void kura_reward_n_kernel(DevParams p_kernarg, const double* __restrict__ x, long long ld,
                                                            const double* __restrict__ ctab,
                                                            const double* __restrict__ stab, int n_bins,
                                                            const double* __restrict__ u0, double* __restrict__ out,
                                                            const double* __restrict__ r2c, int n) {
+    DevParamsK& p = kargs();  // == p_kernarg, read in place (kernarg offset 0)
+    (void)p_kernarg;
     const int j = blockIdx.x;
     if (j >= n) return;
     const int lane = threadIdx.x;
