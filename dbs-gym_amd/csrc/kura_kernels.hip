@@ -57,15 +57,6 @@ __device__ constexpr float kM[7] = {KF(6025192743.0 / 30085553152.0 / 2.0), 0,
                                     KF(187940372067.0 / 1594534317056.0 / 2.0),
                                     KF(-1776094331.0 / 19743644256.0 / 2.0), KF(11237099.0 / 235043384.0 / 2.0)};
 #undef KF
-// same values, addressable with a runtime stage index (scalar loads)
-__constant__ float cA[7][6] = {
-    {0, 0, 0, 0, 0, 0},
-    {kA[1][0], 0, 0, 0, 0, 0},
-    {kA[2][0], kA[2][1], 0, 0, 0, 0},
-    {kA[3][0], kA[3][1], kA[3][2], 0, 0, 0},
-    {kA[4][0], kA[4][1], kA[4][2], kA[4][3], 0, 0},
-    {kA[5][0], kA[5][1], kA[5][2], kA[5][3], kA[5][4], 0},
-    {kA[6][0], kA[6][1], kA[6][2], kA[6][3], kA[6][4], kA[6][5]}};
 
 // Everything a launch needs, passed by value (kernarg).
 struct DevParams {
@@ -643,6 +634,28 @@ __device__ __forceinline__ void coupling_epilogue(DevParamsK& __restrict__ p, co
 // in registers from the epilogue (round 1) only made the compiler spill it
 // across the stage barrier -- 32 dwords per lane per sweep to scratch and
 // back -- and cost 4 % of the step.
+// ys = y0 + chain_j(kA[S][j] * (h f_j)), j < S, zero coefficients skipped
+// (the oracle's order: fp32 products h*f_j, the first term a product, the
+// rest fmas, then y0 + the chain)
+template <int S>
+__device__ __forceinline__ void stage_ys(const float (&y0)[8], const float (&h)[8], const float (&f)[6][8],
+                                         float (&ys)[8]) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        if constexpr (S == 0) {
+            ys[q] = y0[q];
+        } else {
+            float acc = kA[S][0] * (h[q] * f[0][q]);
+            if constexpr (S > 1 && kA[S][1] != 0.0f) acc = __builtin_fmaf(kA[S][1], h[q] * f[1][q], acc);
+            if constexpr (S > 2) acc = __builtin_fmaf(kA[S][2], h[q] * f[2][q], acc);
+            if constexpr (S > 3) acc = __builtin_fmaf(kA[S][3], h[q] * f[3][q], acc);
+            if constexpr (S > 4) acc = __builtin_fmaf(kA[S][4], h[q] * f[4][q], acc);
+            if constexpr (S > 5) acc = __builtin_fmaf(kA[S][5], h[q] * f[5][q], acc);
+            ys[q] = y0[q] + acc;
+        }
+    }
+}
+
 template <int TPW>
 __device__ __forceinline__ void stage_input(const Slot& ws, float* Xs, int s STAMP_PARAMS) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -678,21 +691,18 @@ __device__ __forceinline__ void stage_input(const Slot& ws, float* Xs, int s STA
         const int i = 32 * (wave * TPW + t) + (lane & 31);
         float ys[8];
         int slow = 0;
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-            float v = y0[b][q];
-            if (s > 0) {
-#define KURA_FJ(j) (f[b][j][q])
-                float acc = cA[s][0] * (h[q] * KURA_FJ(0));
-                if (s > 1 && cA[s][1] != 0.0f) acc = __builtin_fmaf(cA[s][1], h[q] * KURA_FJ(1), acc);
-                if (s > 2) acc = __builtin_fmaf(cA[s][2], h[q] * KURA_FJ(2), acc);
-                if (s > 3) acc = __builtin_fmaf(cA[s][3], h[q] * KURA_FJ(3), acc);
-                if (s > 4) acc = __builtin_fmaf(cA[s][4], h[q] * KURA_FJ(4), acc);
-                if (s > 5) acc = __builtin_fmaf(cA[s][5], h[q] * KURA_FJ(5), acc);
-#undef KURA_FJ
-                v = y0[b][q] + acc;
-            }
-            ys[q] = v;
+        // one uniform branch per tile to a chain with the stage's tableau row
+        // as immediates (a runtime-indexed row was a scalar load plus an
+        // lgkmcnt(0) wait per term and element, which also drained the LDS
+        // writes of the tile before)
+        switch (s) {
+            case 0: stage_ys<0>(y0[b], h, f[b], ys); break;
+            case 1: stage_ys<1>(y0[b], h, f[b], ys); break;
+            case 2: stage_ys<2>(y0[b], h, f[b], ys); break;
+            case 3: stage_ys<3>(y0[b], h, f[b], ys); break;
+            case 4: stage_ys<4>(y0[b], h, f[b], ys); break;
+            case 5: stage_ys<5>(y0[b], h, f[b], ys); break;
+            default: stage_ys<6>(y0[b], h, f[b], ys); break;
         }
         // theta = fmod(ys, 2pi_f) folded into the sincos reduction
         // (kdm_sincos_fmod2pi, kura_detmath.h): branch-free for the tile
@@ -1539,7 +1549,7 @@ __device__ KURA_SOLVE_ATTR void solve_wg(DevParamsK& __restrict__ pin, float* Xs
     // (the kernarg segment through the VGPR-passed pointer: vector loads.
     // Made wave-uniform -- scalar loads, which share lgkmcnt with the LDS
     // traffic -- the step was 1.5 % slower in the same-box A/B,
-    // profiles/r04_kargs_ab.txt)
+    // profiles/r04_solver_ab.txt)
     DevParamsK& __restrict__ p = pin;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, tid = threadIdx.x;
     constexpr int N = TPW * 256;            // oscillators owned by this workgroup
