@@ -2015,8 +2015,30 @@ __device__ __forceinline__ void step_pair(DevParamsK& p, Part& pt, float* Xs, co
         const int wp0 = p.wpos[env];
         const WinView xv{rb, e, W, wp0, S};
         STAMP(22);
-        if (obs)
-            for (int i = lane; i < W; i += 64) obs[(size_t)env * W + i] = (float)xv.at(i);
+        if (obs) {  // the new window, oldest first: 8 loads in flight per lane, then 8 stores
+            float* __restrict__ ob = obs + (size_t)env * W;
+            const double* __restrict__ rr = rb;
+            const int keep = W - S;
+#pragma unroll 1
+            for (int i0 = 0; i0 < W; i0 += 64 * 8) {
+                double v[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const int i = i0 + lane + 64 * u;
+                    const int ii = i < keep ? i : 0;       // ring slot of an untouched sample (in range)
+                    int k = wp0 + S + ii;
+                    if (k >= W) k -= W;
+                    const double r = rr[k];
+                    const int j = i < keep ? 0 : (i < W ? i : W - 1) - keep;   // this step's sample (in range)
+                    v[u] = i < keep ? r : s_smp_r[e][j];
+                }
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const int i = i0 + lane + 64 * u;
+                    if (i < W) ob[i] = (float)v[u];
+                }
+            }
+        }
 #ifdef KURA_STAMPS
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #endif

@@ -80,11 +80,19 @@ def test_split_n8192_stress_config(torch_gpu):
     _pair(torch_gpu, 8192, 16, 2)
 
 
-@pytest.mark.parametrize("part,name,reward", [(256, "env0", "bbpow_action"), (512, "env1", "temp_const_action")])
-def test_split_small_parts(torch_gpu, part, name, reward):
-    """Parts of 256 / 512 oscillators (TPW = 1 / 2 split instantiations): the
-    strong-scaling stress form, where few envs per GPU must still fill the CUs."""
-    _pair(torch_gpu, 2048, 19, 3, reward=reward, name=name, part=part)
+@pytest.mark.parametrize("N,part,name,reward", [(2048, 256, "env0", "bbpow_action"),
+                                                 (2048, 512, "env1", "temp_const_action"),
+                                                 (2048, 512, "env0", "bbpow_threth_action"),
+                                                 (2048, 256, "env1", "temp_const_action"),
+                                                 (1024, 512, "env1", "bbpow_action"),
+                                                 (4096, 1024, "env0", "temp_const_action")])
+def test_split_small_parts(torch_gpu, N, part, name, reward):
+    """Parts of 256 / 512 / 1024 oscillators (TPW = 1 / 2 / 4 split
+    instantiations) with both LFP kinds and all rewards: the strong-scaling
+    stress form, where few envs per GPU must still fill the CUs.  (Round 4's
+    lost final state showed only at N = 2048 with parts of 512, DESIGN.md
+    section 5: every instantiation is exercised with both LFP kinds.)"""
+    _pair(torch_gpu, N, 19, 3, reward=reward, name=name, part=part)
 
 
 def test_split_n8192_parts256(torch_gpu):
