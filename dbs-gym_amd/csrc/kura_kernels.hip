@@ -2013,7 +2013,6 @@ __device__ __forceinline__ void step_pair(DevParamsK& p, Part& pt, float* Xs, co
         const int W = p.W;
         double* rb = p.ring + (size_t)env * W;
         const int wp0 = p.wpos[env];
-        const WinView xv{rb, e, W, wp0, S};
         STAMP(22);
         if (obs) {  // the new window, oldest first: 8 loads in flight per lane, then 8 stores
             float* __restrict__ ob = obs + (size_t)env * W;
@@ -2030,7 +2029,11 @@ __device__ __forceinline__ void step_pair(DevParamsK& p, Part& pt, float* Xs, co
                     if (k >= W) k -= W;
                     const double r = rr[k];
                     const int j = i < keep ? 0 : (i < W ? i : W - 1) - keep;   // this step's sample (in range)
-                    v[u] = i < keep ? r : s_smp_r[e][j];
+                    double l = s_smp_r[e][j];
+                    // two loads and a select of values: folded into one load through a selected
+                    // generic pointer, ROCm 7.2's backend fails to select the LDS-aperture check
+                    asm volatile("" : "+v"(l));
+                    v[u] = i < keep ? r : l;
                 }
 #pragma unroll
                 for (int u = 0; u < 8; ++u) {
