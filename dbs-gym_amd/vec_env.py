@@ -53,9 +53,17 @@ class KuraVectorEnv:
                 absent they are drawn as train_aDBS_RL.py:95-112 does, from
                 ``numpy.random.RandomState(w0_seed + b)``.
     rand_seeds: per-env ``rand_seed`` (env.py:291); default params' seed + b.
-    autoreset:  SB3 DummyVecEnv semantics -- a finished env is reset inside the
-                same step() and its last observation is returned in
-                ``infos["terminal_observation"]``.
+    autoreset:  reset finished envs automatically.
+    autoreset_mode: "same_step" (default; SB3 DummyVecEnv semantics) -- a
+                finished env is reset inside the same step() and its last
+                observation is returned in ``infos["terminal_observation"]``;
+                "next_step" (gymnasium 1.x vector envs' default,
+                AutoresetMode.NEXT_STEP) -- the finishing step() returns the
+                env's last observation, and the next step() resets it instead
+                of stepping it (its action is ignored): reset observation,
+                reward 0, terminated/truncated False, ``infos["reset_env_ids"]``.
+                Either way each env's reset draws come from its own stream in
+                the reference's order, so an env's episodes are the same.
     profile:    time the phases of every autoreset (host draws, parameter
                 upload, reset kernel, episode metrics; synchronising) into
                 ``self.boundary_times`` -- bench.py --episode.
@@ -94,7 +102,11 @@ class KuraVectorEnv:
                  w0_seed: int = 228, rand_seeds=None, autoreset: bool = True, max_steps: int = 4096,
                  episode_metrics: bool = False, psd_dt: float = 5e-4, beta_band=(12.5, 21.0),
                  on_failure: str = "raise", profile: bool = False, failure_check: str = "deferred",
-                 max_reset_failures: int = 3):
+                 max_reset_failures: int = 3, autoreset_mode: str = "same_step"):
+        if autoreset_mode not in ("same_step", "next_step"):
+            raise ValueError(f"autoreset_mode={autoreset_mode!r}: expected 'same_step' or 'next_step'")
+        self.autoreset_mode = autoreset_mode
+        self._next_reset = None     # next_step mode: envs that finished in the last step() (reset in the next)
         if on_failure not in ("raise", "reset"):
             raise ValueError(f"on_failure={on_failure!r}: expected 'raise' or 'reset'")
         if failure_check not in ("deferred", "eager"):
@@ -219,6 +231,7 @@ class KuraVectorEnv:
         obs = self.sim.reset(th)
         self._check_reset(None, infos)
         self.steps[:] = 0
+        self._next_reset = None
         self._was_reset = True
         return obs.view(self.num_envs, 1, self.W).clone(), infos
 
@@ -236,6 +249,9 @@ class KuraVectorEnv:
         self._pend = None
         ev.synchronize()
         f = fl.numpy().copy()
+        if rmask is not None and getattr(self, "_pend_discard", None) is not None:
+            f[self._pend_discard] = 0     # next_step mode: those envs' steps were discarded (reset instead)
+        self._pend_discard = None
         idx = np.nonzero(f)[0]
         ridx = np.zeros(0, np.int64)
         if rmask is not None:
@@ -278,6 +294,14 @@ class KuraVectorEnv:
         self.u = lo + ((hi - lo) * (a.double() - x)) / (y - x)      # env.py:389-393 (for callers)
         obs, rew, done = self.sim.step(a)
         self.steps += 1
+        # next_step mode: the envs that finished in the previous call are reset
+        # in this one -- their step above is discarded (the reset below
+        # overwrites its state and outputs)
+        nxt = None
+        if self._next_reset is not None and self._next_reset.any():
+            nxt = np.nonzero(self._next_reset)[0]
+            self.steps[nxt] = 0
+        self._next_reset = None
         term_host = self.steps >= self.episode_steps
         # episode ends from the counters (== the kernel's done for every env whose
         # step succeeded; the kernel also sets done = 1 for a failed env, which is
@@ -288,6 +312,9 @@ class KuraVectorEnv:
             truncated[torch.as_tensor(infos["reset_before_step_ids"], device=self.device)] = True
         if self.failure_check == "eager":
             failed, fflags = self._failures_now()         # synchronises: the step's outputs are ready
+            if nxt is not None:                           # discarded steps do not fail an episode
+                keep = ~np.isin(failed, nxt)
+                failed, fflags = failed[keep], fflags[keep]
             if len(failed):
                 if self.on_failure == "raise":
                     raise KuraSolverError("kura_step", failed.tolist(), fflags.tolist())
@@ -313,7 +340,29 @@ class KuraVectorEnv:
                 ev = self.sim.episode_envelope_stats(mask)
                 infos["episode"]["envelope"] = ev[torch.as_tensor(idx, device=self.device)].cpu().numpy()
             tb["metrics_s"] = time.perf_counter() - t0
-        if self.autoreset and term_host.any():
+        if nxt is not None:   # next_step mode: reset observation, reward 0, not done
+            infos["reset_env_ids"] = nxt
+            mask = torch.zeros(self.num_envs, dtype=torch.uint8)
+            mask[nxt] = 1
+            th = self._draw(nxt)
+            t1 = time.perf_counter()
+            self.sim.reset(th, mask.to(self.device))
+            nxt_dev = torch.as_tensor(nxt, device=self.device)
+            rew[nxt_dev] = 0.0
+            terminated[nxt_dev] = False
+            truncated[nxt_dev] = False
+            if self.failure_check == "eager":
+                self._check_reset(mask)
+            else:
+                self._stash_flags(reset_mask=mask.numpy().astype(bool))
+                self._pend_discard = mask.numpy().astype(bool)
+            if self.profile:
+                torch.cuda.synchronize(self.device)
+            tb.update(n_reset=len(nxt), host_draw_s=self._t_draw, upload_s=self._t_upload,
+                      reset_kernel_s=time.perf_counter() - t1)
+        if self.autoreset and self.autoreset_mode == "next_step" and term_host.any():
+            self._next_reset = term_host.copy()
+        if self.autoreset and self.autoreset_mode == "same_step" and term_host.any():
             infos["terminal_observation"] = obs[torch.as_tensor(idx, device=self.device)].clone().view(-1, 1, self.W)
             mask = torch.zeros(self.num_envs, dtype=torch.uint8)
             mask[idx] = 1

@@ -148,3 +148,9 @@ def test_reset_draws_batch_replay_hosts():
         for k, x in enumerate(d):
             for got, want in zip((w0[k], gs[k], gr[k], th[k]), x[r]):
                 np.testing.assert_array_equal(got, want)
+
+
+def test_autoreset_mode_is_validated():
+    vec = importlib.import_module("dbs-gym_amd.vec_env")
+    with pytest.raises(ValueError, match="autoreset_mode"):
+        vec.KuraVectorEnv(kura.reference_params("env0"), num_envs=1, autoreset_mode="final_obs")

@@ -123,3 +123,69 @@ def test_env2_drift_and_per_env_K(torch_gpu):
             np.testing.assert_array_equal(obs[:, 0].cpu().numpy(), ref["obs"])
     np.testing.assert_array_equal(env.sim.get_state()["y"], o.state()["y"])
     env.close()
+
+
+def _run_modes(vec, p, mode, B, ncalls, offsets):
+    """Per env and (episode, step): the observation and reward a KuraVectorEnv
+    in the given autoreset mode returns; (b, e, 'reset'): the reset
+    observation that opens episode e."""
+    env = vec.KuraVectorEnv(p, num_envs=B, reward_func="bbpow_action", autoreset_mode=mode)
+    env.episode_steps = 3
+    env.reset()
+    env.steps[:] = offsets              # envs finish in different calls
+    pos = [[0, int(o)] for o in offsets]
+    rec, pending = {}, set()
+
+    def act(b, e, j):
+        return np.random.default_rng(1000 * b + 10 * e + j).uniform(-1, 1)
+
+    for _ in range(ncalls):
+        a = np.array([[act(b, *pos[b])] for b in range(B)], np.float32)
+        obs, rew, term, trunc, info = env.step(a)
+        o_np, r_np, t_np = obs[:, 0].cpu().numpy(), rew.cpu().numpy(), term.cpu().numpy()
+        assert not trunc.cpu().numpy().any()
+        for b in range(B):
+            e, j = pos[b]
+            if b in pending:               # next_step: this call reset env b (its action ignored)
+                assert r_np[b] == 0.0 and not t_np[b] and b in info["reset_env_ids"]
+                rec[(b, e + 1, "reset")] = o_np[b]
+                pending.discard(b)
+                pos[b] = [e + 1, 0]
+            elif j == 2:                   # the episode's last step
+                assert t_np[b]
+                if mode == "same_step":
+                    k = list(info["terminal_env_ids"]).index(b)
+                    rec[(b, e, j)] = (info["terminal_observation"][k, 0].cpu().numpy(), r_np[b])
+                    rec[(b, e + 1, "reset")] = o_np[b]
+                    pos[b] = [e + 1, 0]
+                else:
+                    assert "terminal_observation" not in info
+                    rec[(b, e, j)] = (o_np[b], r_np[b])
+                    pending.add(b)
+                    pos[b] = [e, 3]
+            else:
+                assert not t_np[b]
+                rec[(b, e, j)] = (o_np[b], r_np[b])
+                pos[b] = [e, j + 1]
+    env.close()
+    return rec
+
+
+def test_next_step_autoreset_mode_matches_same_step(torch_gpu):
+    """gymnasium's NEXT_STEP autoreset: the finishing call returns the last
+    observation, the next call resets the env (reward 0, not done) -- every
+    env's episodes identical, step for step, to SB3's same-step mode (checked
+    against the oracle above), with envs finishing in different calls."""
+    vec = importlib.import_module("dbs-gym_amd.vec_env")
+    p = kura.reference_params("env0", "eval", 1)
+    B, offsets = 4, [0, 1, 2, 2]
+    same = _run_modes(vec, p, "same_step", B, 8, offsets)
+    nxt = _run_modes(vec, p, "next_step", B, 11, offsets)
+    common = set(same) & set(nxt)
+    assert len(common) >= 4 * 7 and sum(1 for k in common if k[2] == "reset") >= 4 * 2
+    for k in common:
+        if k[2] == "reset":
+            np.testing.assert_array_equal(nxt[k], same[k])
+        else:
+            np.testing.assert_array_equal(nxt[k][0], same[k][0])
+            assert nxt[k][1] == same[k][1]
