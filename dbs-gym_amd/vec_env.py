@@ -165,6 +165,7 @@ class KuraVectorEnv:
         # deferred failure flags: pinned host copies of the last step's and the
         # last autoreset's per-env flags, and the events that complete them
         self._pend = None          # (flags_pinned, event, reset_mask or None, reset_flags_pinned)
+        self._pend_discard = None  # next_step mode: envs whose step in that launch was discarded
         self._reset_fail_runs = np.zeros(B, np.int64)   # consecutive failed resets per env
         self._pending_gain = {}    # env -> float32(K/N) of a set_attr'd params_dict, applied at its next reset
         self._omega = np.zeros((B, self.N), np.float32)
@@ -249,7 +250,7 @@ class KuraVectorEnv:
         self._pend = None
         ev.synchronize()
         f = fl.numpy().copy()
-        if rmask is not None and getattr(self, "_pend_discard", None) is not None:
+        if rmask is not None and self._pend_discard is not None:
             f[self._pend_discard] = 0     # next_step mode: those envs' steps were discarded (reset instead)
         self._pend_discard = None
         idx = np.nonzero(f)[0]
