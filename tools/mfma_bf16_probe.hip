@@ -12,7 +12,7 @@
 // 8 bf16 of lane l; D value j of lane l at row (j%4) + 8*(j/4) + 4*(l/32),
 // column l%32.  (Only the seq_* models depend on the k order.)
 //   hipcc --offload-arch=gfx950 -O2 -o tools/mfma_bf16_probe tools/mfma_bf16_probe.hip
-//   ./mfma_bf16_probe [trials]
+//   ./mfma_bf16_probe [trials] [dump.bin]
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
@@ -116,5 +116,14 @@ int main(int argc, char** argv) {
     }
     printf("trials %d: exact %ld  seq_k %ld  seq_rk %ld  sum_c %ld  any %ld\n", trials, m_exact, m_seqk, m_seqr,
            m_sumc, m_any);
+    if (argc > 2) {   // raw dump for offline model fitting: x, y (uint16 x 16 per trial), c, gpu (f32 per trial)
+        FILE* f = fopen(argv[2], "wb");
+        if (!f) return 1;
+        fwrite(hx, 2, (size_t)trials * 16, f);
+        fwrite(hy, 2, (size_t)trials * 16, f);
+        fwrite(hc, 4, (size_t)trials, f);
+        fwrite(ho, 4, (size_t)trials, f);
+        fclose(f);
+    }
     return 0;
 }
