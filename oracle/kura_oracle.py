@@ -196,6 +196,18 @@ def sincos(x):
     return s, c
 
 
+def mfma_bf16_dot16(x_bf16, y_bf16, c):
+    """oracle_mfma_bf16_dot16 for each row of x, y (uint16 bf16 bit patterns,
+    (n, 16)) and c (n,): the gfx950 bf16 MFMA's accumulation model."""
+    L = lib()
+    f = L.oracle_mfma_bf16_dot16
+    f.restype = ctypes.c_float
+    f.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_float]
+    x = np.ascontiguousarray(x_bf16, np.uint16)
+    y = np.ascontiguousarray(y_bf16, np.uint16)
+    return np.array([f(x[t].ctypes.data, y[t].ctypes.data, float(c[t])) for t in range(len(c))], np.float32)
+
+
 def sincos_fmod2pi(x):
     """sin, cos of fmod(x, 2pi_f) as the RHS takes them (kdm_sincos_fmod2pi)"""
     x = np.ascontiguousarray(x, np.float32)
