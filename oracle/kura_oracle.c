@@ -897,3 +897,17 @@ float oracle_mfma_bf16_dot16(const uint16_t* x, const uint16_t* y, float c) {
     }
     return acc;
 }
+
+/* One output of a coupling GEMM computed from three-way bf16 splits
+ * (x = x1 + x2 + x3, a = a1 + a2 + a3; xp, ap: [3][K] bf16 bit patterns) on
+ * the bf16 MFMA: per 16-deep k-block the six part products x1a1, x1a2, x2a1,
+ * x1a3, x2a2, x3a1 in that order, each one oracle_mfma_bf16_dot16 into the
+ * running f32 accumulator (from +0).  The order of tools/split_gemm_bench.hip's
+ * mfma6; groundwork, not used by the shipped kernel. */
+float oracle_split_bf16_chain(const uint16_t* xp, const uint16_t* ap, int K) {
+    static const int pi[6] = {0, 0, 1, 0, 1, 2}, pj[6] = {0, 1, 0, 2, 1, 0};
+    float acc = 0.0f;
+    for (int kb = 0; kb + 16 <= K; kb += 16)
+        for (int q = 0; q < 6; ++q) acc = oracle_mfma_bf16_dot16(xp + (size_t)pi[q] * K + kb, ap + (size_t)pj[q] * K + kb, acc);
+    return acc;
+}

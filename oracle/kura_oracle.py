@@ -208,6 +208,19 @@ def mfma_bf16_dot16(x_bf16, y_bf16, c):
     return np.array([f(x[t].ctypes.data, y[t].ctypes.data, float(c[t])) for t in range(len(c))], np.float32)
 
 
+def split_bf16_chain(xp, ap):
+    """oracle_split_bf16_chain for each row: xp, ap (n, 3, K) bf16 bit patterns
+    of the split operands -> (n,) float32 (the split GEMM's accumulation)."""
+    L = lib()
+    f = L.oracle_split_bf16_chain
+    f.restype = ctypes.c_float
+    f.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+    xp = np.ascontiguousarray(xp, np.uint16)
+    ap = np.ascontiguousarray(ap, np.uint16)
+    K = xp.shape[2]
+    return np.array([f(xp[t].ctypes.data, ap[t].ctypes.data, K) for t in range(len(xp))], np.float32)
+
+
 def sincos_fmod2pi(x):
     """sin, cos of fmod(x, 2pi_f) as the RHS takes them (kdm_sincos_fmod2pi)"""
     x = np.ascontiguousarray(x, np.float32)

@@ -14,7 +14,10 @@
 // f32_table == f32_stream and split_table == split_stream bit for bit (same
 // operands, same order); the split forms are compared with the exact sum.
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -o tools/split_gemm_bench tools/split_gemm_bench.hip
-//   ./tools/split_gemm_bench [reps]
+//   ./tools/split_gemm_bench [reps] [dump.bin]
+// dump.bin: split_stream's outputs of workgroup 0 (512 threads x 4 tiles x 16
+// floats, the raw accumulator layout) for tools/split_gemm_check.py, which
+// recomputes them with the oracle's exact bf16 MFMA model
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
@@ -387,6 +390,12 @@ int main(int argc, char** argv) {
                     s2 += a2;
                     ++cnt;
                 }
+    if (argc > 2) {
+        FILE* f = fopen(argv[2], "wb");
+        if (!f) return 1;
+        fwrite(res[2].data(), 4, (size_t)NT * TPW * 16, f);
+        fclose(f);
+    }
     printf("|error| vs exact over %ld outputs: f32 max %.3g mean %.3g; split max %.3g mean %.3g\n", cnt, e0, s0 / cnt,
            e2, s2 / cnt);
     return 0;
