@@ -1390,11 +1390,9 @@ __device__ __forceinline__ int post_step(DevParamsK& __restrict__ p, Slot& ws, i
     // slower in the same-box A/B -- the fused epilogue holds the
     // accumulators and the seven records of a tile at once)
     float part[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-#ifdef KURA_ERR_UNROLL
-#pragma unroll
-#else
+    // (kept rolled: the unrolled loop measured 0.4 % slower, same box,
+    // profiles/r04_solver_ab.txt)
 #pragma unroll 1
-#endif
     for (int t = 0; t < TPW; ++t) {
         float y0[8], y1[8], f0[8], f2[8], f3[8], f4[8], f5[8], f6[8];
         load8(ws, SL_Y0, t, y0);

@@ -14,7 +14,7 @@
 // f32_table == f32_stream and split_table == split_stream bit for bit (same
 // operands, same order); the split forms are compared with the exact sum.
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -o tools/split_gemm_bench tools/split_gemm_bench.hip
-//   ./tools/split_gemm_bench [reps] [dump.bin]
+//   ./tools/split_gemm_bench [reps] [dump.bin] [trace.bin]
 // dump.bin: split_stream's outputs of workgroup 0 (512 threads x 4 tiles x 16
 // floats, the raw accumulator layout) for tools/split_gemm_check.py, which
 // recomputes them with the oracle's exact bf16 MFMA model
@@ -249,6 +249,31 @@ __global__ __launch_bounds__(NT) void gemm(const float* __restrict__ gA, const u
         for (int r = 0; r < 16; ++r) out[((size_t)(blockIdx.x * NT + tid) * TPW + t) * 16 + r] = acc[t][r];
 }
 
+// Trace of one 32x32 tile's split chain (column tile 0, workgroup 0's
+// operand): the accumulator after every one of the NKB*6 MFMAs, so a model
+// mismatch can be pinned to the first MFMA (and its A, B, C) that departs.
+__global__ __launch_bounds__(64) void trace(const uint16_t* __restrict__ gS, float* __restrict__ tr) {
+    const int lane = threadIdx.x;
+    f32x16 acc;
+    for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
+    const u32x4* sp = reinterpret_cast<const u32x4*>(gS);   // tile 0: [kb][p][lane] 16 B
+    for (int kb = 0; kb < NKB; ++kb) {
+        f32x4 lo, hi;
+        for (int c = 0; c < 4; ++c) {
+            lo[c] = operand(lane & 31, kb * 16 + 8 * (lane >> 5) + c, 0);
+            hi[c] = operand(lane & 31, kb * 16 + 8 * (lane >> 5) + 4 + c, 0);
+        }
+        bf16x8 x[3], a[3];
+        split8(lo, hi, x[0], x[1], x[2]);
+        for (int p = 0; p < 3; ++p) a[p] = __builtin_bit_cast(bf16x8, sp[(kb * 3 + p) * 64 + lane]);
+        const int pi[6] = {0, 0, 1, 0, 1, 2}, pj[6] = {0, 1, 0, 2, 1, 0};
+        for (int q = 0; q < 6; ++q) {
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x[pi[q]], a[pj[q]], acc, 0, 0, 0);
+            for (int r = 0; r < 16; ++r) tr[((size_t)(kb * 6 + q) * 64 + lane) * 16 + r] = acc[r];
+        }
+    }
+}
+
 // ---------------------------------------------------------------- host ----
 static uint16_t bf16_rne(float f) {
     uint32_t u;
@@ -394,6 +419,18 @@ int main(int argc, char** argv) {
         FILE* f = fopen(argv[2], "wb");
         if (!f) return 1;
         fwrite(res[2].data(), 4, (size_t)NT * TPW * 16, f);
+        fclose(f);
+    }
+    if (argc > 3) {
+        float* dTr;
+        const size_t trn = (size_t)NKB * 6 * 64 * 16;
+        hipMalloc(&dTr, trn * 4);
+        hipLaunchKernelGGL(trace, dim3(1), dim3(64), 0, 0, dS, dTr);
+        std::vector<float> htr(trn);
+        hipMemcpy(htr.data(), dTr, trn * 4, hipMemcpyDeviceToHost);
+        FILE* f = fopen(argv[3], "wb");
+        if (!f) return 1;
+        fwrite(htr.data(), 4, trn, f);
         fclose(f);
     }
     printf("|error| vs exact over %ld outputs: f32 max %.3g mean %.3g; split max %.3g mean %.3g\n", cnt, e0, s0 / cnt,
