@@ -208,11 +208,23 @@ def mfma_bf16_dot16(x_bf16, y_bf16, c):
     return np.array([f(x[t].ctypes.data, y[t].ctypes.data, float(c[t])) for t in range(len(c))], np.float32)
 
 
-def split_bf16_chain(xp, ap):
-    """oracle_split_bf16_chain for each row: xp, ap (n, 3, K) bf16 bit patterns
-    of the split operands -> (n,) float32 (the split GEMM's accumulation)."""
+def mfma_bf16_dot16_i64(x_bf16, y_bf16, c):
+    """oracle_mfma_bf16_dot16_i64: the same model in int64 arithmetic."""
     L = lib()
-    f = L.oracle_split_bf16_chain
+    f = L.oracle_mfma_bf16_dot16_i64
+    f.restype = ctypes.c_float
+    f.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_float]
+    x = np.ascontiguousarray(x_bf16, np.uint16)
+    y = np.ascontiguousarray(y_bf16, np.uint16)
+    return np.array([f(x[t].ctypes.data, y[t].ctypes.data, float(c[t])) for t in range(len(c))], np.float32)
+
+
+def split_bf16_chain(xp, ap, i64=False):
+    """oracle_split_bf16_chain (or its int64 form) for each row: xp, ap
+    (n, 3, K) bf16 bit patterns of the split operands -> (n,) float32 (the
+    split GEMM's accumulation)."""
+    L = lib()
+    f = L.oracle_split_bf16_chain_i64 if i64 else L.oracle_split_bf16_chain
     f.restype = ctypes.c_float
     f.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
     xp = np.ascontiguousarray(xp, np.uint16)

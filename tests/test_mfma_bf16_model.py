@@ -75,3 +75,30 @@ def test_split_gemm_outputs_equal_the_oracle_chain():
     as_ = chk.split3(chk.alpha_matrix().T.copy())
     want = ko.split_bf16_chain(xs[row], as_[col])
     assert np.array_equal(want.view(np.uint32), d["gpu"].view(np.uint32))
+    # the int64 / AVX2 form the solver oracle will use (round 5) as well
+    want = ko.split_bf16_chain(xs[row], as_[col], i64=True)
+    assert np.array_equal(want.view(np.uint32), d["gpu"].view(np.uint32))
+
+
+def test_int64_form_equals_the_int128_restatement():
+    """oracle_mfma_bf16_dot16_i64 (int64, AVX2 group sums) == the int128
+    restatement on both hardware fixtures and on 100 000 random dots over a
+    wide exponent range with zeros and accumulators from 2^-30 to 2^30."""
+    from oracle import kura_oracle as ko
+    for name in ("mfma_bf16_probe.npz", "mfma_bf16_chain_cases.npz"):
+        d = np.load(os.path.join(ROOT, "tests", "golden", name))
+        got = ko.mfma_bf16_dot16_i64(d["x_bf16"], d["y_bf16"], d["c"])
+        assert np.array_equal(got.view(np.uint32), d["gpu"].view(np.uint32)), name
+    rng = np.random.default_rng(11)
+    n = 100_000
+
+    def rb(lo, hi):
+        e, m, s = rng.integers(lo, hi, (n, 16)), rng.integers(0, 128, (n, 16)), rng.integers(0, 2, (n, 16))
+        v = ((s << 15) | ((e + 127) << 7) | m).astype(np.uint16)
+        v[rng.random((n, 16)) < 0.1] = 0
+        return v
+    x, y = rb(-40, 10), rb(-20, 10)
+    c = (rng.standard_normal(n) * np.exp2(rng.integers(-30, 30, n))).astype(np.float32)
+    c[::7] = 0
+    a, b = ko.mfma_bf16_dot16(x, y, c), ko.mfma_bf16_dot16_i64(x, y, c)
+    assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
