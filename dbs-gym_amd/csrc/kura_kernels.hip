@@ -228,6 +228,81 @@ __device__ __forceinline__ T* uniform_ptr(T* ptr) {
 }
 
 
+#ifdef KURA_SPLIT_GEMM
+// EXPERIMENT (built only as libkura_split.so for a
+// same-box timing A/B -- the oracle does not model it, so no parity test
+// runs it): the coupling from three-way bf16 splits on
+// v_mfma_f32_32x32x16_bf16, six part products per 16-deep k-block.  alpha
+// arrives pre-split (kura_set_coupling under the same macro): per column
+// tile jt, k-block b and part p, lane l holds 8 bf16 at k = 16b + 8(i/4) +
+// 2(i%4) + l/32 -- the k order of the fp32 operand image, so the sin/cos
+// rows are split from the same two float4 reads.
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ void split_bf16x3(floatx4 lo, floatx4 hi, bf16x8& h1, bf16x8& h2, bf16x8& h3) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const float x = i < 4 ? lo[i] : hi[i - 4];
+        const __bf16 a = (__bf16)x;
+        const float r1 = x - (float)a;
+        const __bf16 b = (__bf16)r1;
+        h1[i] = a;
+        h2[i] = b;
+        h3[i] = (__bf16)(r1 - (float)b);
+    }
+}
+
+template <int TPW>
+__device__ __forceinline__ void coupling_gemm(const float* __restrict__ Xs, const float* __restrict__ alpha_sw,
+                                              floatx16 (&acc)[TPW], unsigned long long* dbg = nullptr) {
+    (void)dbg;
+    constexpr int N = TPW * 32 * NWAVES;
+    constexpr int NB = N / 16;
+    constexpr int TSTRIDE = NB * 3 * 64 * 16;   // bytes per column tile
+    int lane;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+#pragma unroll
+    for (int t = 0; t < TPW; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[t][r] = 0.0f;
+    const floatx4* xs4 = reinterpret_cast<const floatx4*>(Xs + (lane >> 5) * XS_HALF + (lane & 31) * 4);
+    const float* au = uniform_ptr(alpha_sw);
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)((const char*)au + (size_t)wave * TPW * TSTRIDE), 0, TPW * TSTRIDE, 0x00020000);
+    auto ld = [&](int t, int b, int p) -> bf16x8 {
+        return __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rs, ((b * 3 + p) * 64 + lane) * 16,
+                                                                                 t * TSTRIDE, 0));
+    };
+    // one register set per tile, refilled with the next k-block right after
+    // its six MFMAs (cover: the other tiles' MFMAs and the partner wave's)
+    bf16x8 a1[TPW], a2[TPW], a3[TPW];
+#pragma unroll
+    for (int t = 0; t < TPW; ++t) {
+        a1[t] = ld(t, 0, 0);
+        a2[t] = ld(t, 0, 1);
+        a3[t] = ld(t, 0, 2);
+    }
+#pragma unroll 1
+    for (int b = 0; b < NB; ++b) {
+        bf16x8 x1, x2, x3;
+        split_bf16x3(xs4[(2 * b) * (XS_BLOCK / 4)], xs4[(2 * b + 1) * (XS_BLOCK / 4)], x1, x2, x3);
+        const int bn = b + 1 < NB ? b + 1 : NB - 1;
+#pragma unroll
+        for (int t = 0; t < TPW; ++t) {
+            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x1, a1[t], acc[t], 0, 0, 0);
+            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x1, a2[t], acc[t], 0, 0, 0);
+            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x2, a1[t], acc[t], 0, 0, 0);
+            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x1, a3[t], acc[t], 0, 0, 0);
+            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x2, a2[t], acc[t], 0, 0, 0);
+            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x3, a1[t], acc[t], 0, 0, 0);
+            a1[t] = ld(t, bn, 0);
+            a2[t] = ld(t, bn, 1);
+            a3[t] = ld(t, bn, 2);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+#else
 // wave w owns column tiles w*TPW .. w*TPW+TPW-1
 template <int TPW>
 __device__ __forceinline__ void coupling_gemm(const float* __restrict__ Xs, const float* __restrict__ alpha_sw,
@@ -297,6 +372,7 @@ __device__ __forceinline__ void coupling_gemm(const float* __restrict__ Xs, cons
         __builtin_amdgcn_sched_barrier(0);
     }
 }
+#endif  // KURA_SPLIT_GEMM
 
 // Workgroup barrier that orders LDS only.  Inside a solve every workspace
 // record (R) is written and read back by the same lane (MFMA-layout
