@@ -212,10 +212,15 @@ int oracle_arange(double start, double stop, double step, double* out, int cap) 
 }
 
 /* --------------------------------------------------------------- context */
+void* oracle_split_prepare(const float* A, int N, int K);
+void oracle_split_free(void* p);
+void oracle_split_gemm_rows(const void* prep, const float* X, int R, float* Y);
+
 typedef struct {
     KuraConfig cfg;
     int N;
     float* alphaT; /* alphaT[j*N + i] = alpha[i][j] */
+    void* split;   /* oracle_set_split: alpha's bf16 parts -- the split-bf16 coupling (KURA_SPLIT_GEMM builds) */
     float* kn_env; /* per-env float32(K/N) (oracle_set_gain), NULL -> cfg.kn */
     int kn_n;
     int part;      /* split-group part width (N > 1024): cfg.part_osc or 1024 */
@@ -242,7 +247,28 @@ void oracle_destroy(void* p) {
     if (!o) return;
     free(o->alphaT);
     free(o->kn_env);
+    oracle_split_free(o->split);
     free(o);
+}
+
+/* Coupling arithmetic of the KURA_SPLIT_GEMM build:
+ * P, Q from three-way bf16 splits on the bf16 MFMA's exact accumulation
+ * (oracle_split_gemm_rows) instead of the fp32 fmaf chain.  N <= 1024 (the
+ * split build refuses split groups). */
+int oracle_set_split(void* ctx, int on) {
+    OCtx* o = (OCtx*)ctx;
+    oracle_split_free(o->split);
+    o->split = NULL;
+    if (!on) return KURA_OK;
+    const int N = o->N;
+    if (N > 1024 || N % 16) return KURA_E_UNSUPPORTED;
+    float* A = (float*)malloc(sizeof(float) * (size_t)N * N);
+    if (!A) return KURA_E_NOMEM;
+    for (int j = 0; j < N; ++j)
+        for (int i = 0; i < N; ++i) A[(size_t)i * N + j] = o->alphaT[(size_t)j * N + i];
+    o->split = oracle_split_prepare(A, N, N);
+    free(A);
+    return o->split ? KURA_OK : KURA_E_NOMEM;
 }
 
 /* Per-env coupling gain float32(K_b / N) (each env's params_dict['K'],
@@ -266,6 +292,7 @@ typedef struct {
     float *row;           /* a saved row */
     float *cosrow;
     float *zero;          /* pulse = 0 (stim OFF), env.py:434 */
+    float *sc, *pq;       /* split coupling: [s; c] in, [P; Q] out (2N each) */
     double *prod;
     float kn;             /* coupling gain of the env being solved */
 } Work;
@@ -282,14 +309,18 @@ static int work_alloc(Work* w, int N) {
         w->F[k] = (float*)malloc(sizeof(float) * nf);
         if (!w->F[k]) return -1;
     }
+    w->sc = (float*)malloc(sizeof(float) * 2 * nf);
+    w->pq = (float*)malloc(sizeof(float) * 2 * nf);
     w->prod = (double*)malloc(sizeof(double) * nf);
-    return w->prod ? 0 : -1;
+    return (w->prod && w->sc && w->pq) ? 0 : -1;
 }
 
 static void work_free(Work* w) {
     float* fl[] = {w->s, w->c, w->P, w->Q, w->y0, w->ys, w->y1, w->ca, w->cb, w->cc, w->row, w->cosrow, w->zero};
     for (size_t i = 0; i < sizeof(fl) / sizeof(fl[0]); ++i) free(fl[i]);
     for (int k = 0; k < 7; ++k) free(w->F[k]);
+    free(w->sc);
+    free(w->pq);
     free(w->prod);
 }
 
@@ -306,7 +337,14 @@ static void rhs(const OCtx* o, Work* w, const float* y, const float* omega, cons
     const int N = o->N;
     for (int j = 0; j < N; ++j) kdm_sincos_fmod2pi(y[j], &w->s[j], &w->c[j]);   /* theta = fmod(y, 2pi_f) */
     enum { IB = 256 };
-    for (int ib = 0; ib < N; ib += IB) {
+    if (o->split) {   /* the KURA_SPLIT_GEMM build's coupling */
+        memcpy(w->sc, w->s, sizeof(float) * N);
+        memcpy(w->sc + N, w->c, sizeof(float) * N);
+        oracle_split_gemm_rows(o->split, w->sc, 2, w->pq);
+        memcpy(w->P, w->pq, sizeof(float) * N);
+        memcpy(w->Q, w->pq + N, sizeof(float) * N);
+    }
+    for (int ib = 0; ib < N && !o->split; ib += IB) {
         int ie = ib + IB < N ? ib + IB : N;
         float Pb[IB], Qb[IB];
         for (int i = ib; i < ie; ++i) { Pb[i - ib] = 0.0f; Qb[i - ib] = 0.0f; }
