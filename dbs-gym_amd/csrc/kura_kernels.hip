@@ -273,8 +273,6 @@ __device__ __forceinline__ void coupling_gemm(const float* __restrict__ Xs, cons
         return __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rs, ((b * 3 + p) * 64 + lane) * 16,
                                                                                  t * TSTRIDE, 0));
     };
-    // one register set per tile, refilled with the next k-block right after
-    // its six MFMAs (cover: the other tiles' MFMAs and the partner wave's)
     bf16x8 a1[TPW], a2[TPW], a3[TPW];
 #pragma unroll
     for (int t = 0; t < TPW; ++t) {
@@ -282,6 +280,8 @@ __device__ __forceinline__ void coupling_gemm(const float* __restrict__ Xs, cons
         a2[t] = ld(t, 0, 1);
         a3[t] = ld(t, 0, 2);
     }
+    // one register set per tile, refilled with the next k-block right after
+    // its six MFMAs (cover: the other tiles' MFMAs and the partner wave's)
 #pragma unroll 1
     for (int b = 0; b < NB; ++b) {
         bf16x8 x1, x2, x3;
