@@ -25,7 +25,7 @@ N = 1024
 perm = (np.arange(N).reshape(-1, 16)[:, np.r_[0:16:2, 1:16:2]]).ravel()
 tot = bad_n = 0
 for seed in range(n):
-    rng = np.random.default_rng(1000 + seed)
+    rng = np.random.default_rng(int(os.environ.get("HUNT_BASE", "1000")) + seed)
     th = rng.uniform(0, 2 * np.pi, (16, N)).astype(np.float32)
     X = np.concatenate([np.sin(th), np.cos(th)]).astype(np.float32)
     kind = seed % 3
