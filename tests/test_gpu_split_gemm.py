@@ -105,6 +105,41 @@ def test_split_step_parity(torch_gpu, name, N, reward, act):
     _run_from_common_state(torch_gpu, name, N, 4, reward, 3, act)
 
 
+def _run_pair(torch, name, N, B, reward, steps, act, **overrides):
+    """reset (the transient: ~10^7 modelled MFMA outputs) and steps, both
+    sides in split arithmetic from theta0: bit-exact throughout."""
+    sim_mod = importlib.import_module("dbs-gym_amd.sim")
+    cfg, alpha, omega, gs, gr, th0, ct, st, _ = make_case(name, N, B, reward=reward, **overrides)
+    sim = sim_mod.KuraSim(cfg, 0, lib_path=SPLIT_LIB)
+    sim.set_coupling(alpha)
+    sim.set_env_params(omega, gs, gr)
+    sim.set_spectral(ct, st)
+    o = ko.Oracle(cfg, alpha)
+    o.set_split(True)
+    o.set_env_params(omega, gs, gr)
+    o.set_spectral(ct, st)
+    np.testing.assert_array_equal(sim.reset(torch.from_numpy(th0)).cpu().numpy(), o.reset(th0))
+    _cmp_state(sim.get_state(), o.state(), "reset")
+    for k in range(steps):
+        a = actions(act, B, cfg.n_elec, k)
+        sim.step(torch.from_numpy(a))
+        ref = o.step(a)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(sim.obs.cpu().numpy(), ref["obs"])
+        np.testing.assert_array_equal(sim.reward.cpu().numpy(), ref["reward"])
+        _cmp_state(sim.get_state(), o.state(), f"step {k}")
+    sim.close()
+
+
+@pytest.mark.parametrize("name,N,reward,act", [
+    ("env0", 1024, "bbpow_action", "rand"),
+    ("env1", 512, "bbpow_threth_action", "hf"),
+    ("env0", 256, "bbpow_action", "off"),
+])
+def test_split_reset_and_step_parity(torch_gpu, name, N, reward, act):
+    _run_pair(torch_gpu, name, N, 4, reward, 4, act)
+
+
 def test_split_refuses_split_groups(torch_gpu):
     """n_osc > 1024 (the fp32 split-group path) is refused, not run wrong."""
     sim_mod = importlib.import_module("dbs-gym_amd.sim")
