@@ -1,8 +1,8 @@
 """The split-bf16 coupling build (libkura_split.so, -DKURA_SPLIT_GEMM;
 DESIGN.md section 9) is a twin of the oracle in its split mode
 (Oracle.set_split: oracle_split_gemm_rows, the bf16 MFMA's exact
-accumulation over three-way bf16 splits): its GEMM and its steps bit-exact
-(from a common state), as the shipped fp32 build is against the fmaf-chain
+accumulation over three-way bf16 splits): its GEMM, its reset transients and
+its steps bit-exact, as the shipped fp32 build is against the fmaf-chain
 oracle (tests/test_gpu_parity.py).
 Not the product path yet -- the experiment's parity gate (round 5 switches
 the product once the long-horizon gates are re-planned around the split
@@ -43,10 +43,7 @@ def _cmp_state(g, o, where):
 
 def _run_from_common_state(torch, name, N, B, reward, steps, act, **overrides):
     """Both sides start from the fp32 oracle's reset state (kura_set_state),
-    then step with the split coupling: every step bit-exact.  (The split
-    reset transient itself is not yet a twin: over its ~10^7 modelled MFMA
-    outputs a rare case of the accumulation model still parts the two,
-    DESIGN.md section 9.)"""
+    then step with the split coupling: every step bit-exact."""
     sim_mod = importlib.import_module("dbs-gym_amd.sim")
     cfg, alpha, omega, gs, gr, th0, ct, st, _ = make_case(name, N, B, reward=reward, **overrides)
     base = ko.Oracle(cfg, alpha)
