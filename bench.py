@@ -33,7 +33,11 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 PEAK_FP32_TFLOPS = 157.3   # MI355X dense FP32 (vector == matrix), MI355X_MICROARCH.md
+PEAK_BF16_TFLOPS = 2516.6  # MI355X dense BF16 MFMA (1024 FLOP/clk/SIMD x 1024 SIMDs x 2.4 GHz; "~2.5 PF dense")
 PEAK_HBM_GBS = 8000.0
+# KURA_COUPLING_BF16X3 executes six bf16 products per fp32 product of the coupling
+# (x1a1, x1a2, x2a1, x1a3, x2a2, x3a1; kura.h)
+BF16X3_PRODUCTS = 6
 
 
 def parse(argv=None):
@@ -55,6 +59,8 @@ def parse(argv=None):
     ap.add_argument("--episode-metrics", action="store_true",
                     help="--episode with episode_metrics=True (beta power + envelope of every finished episode)")
     ap.add_argument("--reward", default="bbpow_action")
+    ap.add_argument("--coupling", default="auto", choices=["auto", "f32", "bf16x3"],
+                    help="coupling arithmetic (kura.h KURA_COUPLING_*; auto = bf16x3 for N <= 1024, f32 above)")
     ap.add_argument("--cpu-seconds", type=float, default=24.0,
                     help="bounded CPU-baseline budget in seconds (0 = skip), split over its legs")
     ap.add_argument("--seed", type=int, default=2024)
@@ -88,7 +94,7 @@ def build_shard(args, rank):
     omega, g_stim, g_rec, theta0 = kura.reset_arrays(hosts)
     cfg = sim_mod.make_config(base, B, reward_func=args.reward,
                               part_osc=(sim_mod.auto_part_osc(args.osc, B) if getattr(args, "part_osc", -1) < 0
-                                        else args.part_osc))
+                                        else args.part_osc), coupling=getattr(args, "coupling", "auto"))
     bins = kura.spectral.beta_bins(cfg.window, base["verbose_dt"])
     ctab, stab = kura.spectral.twiddles(cfg.window, bins)
     return cfg, shared["alpha"].astype(np.float32), omega, g_stim, g_rec, theta0, ctab, stab, shared["gain"]
@@ -155,6 +161,7 @@ def _ref_env(args, n_osc):
     import copy
     a = copy.copy(args)
     a.osc, a.envs, a.random_k = n_osc, 1, False
+    a.coupling = "f32"   # only the starting state: the reference op sequence runs its own (direct-sin) arithmetic
     cfg, alpha, omega, gs, gr, th0, ct, st, gain = build_shard(a, 0)
     o = ko.Oracle(cfg, alpha)
     o.set_env_params(omega, gs, gr)
@@ -209,15 +216,17 @@ def cpu_baseline(args):
     return out
 
 
-def kernel_name(N, part=0):
+def kernel_name(N, part=0, coupling="f32"):
     """The step kernel instantiation libkura launches for N oscillators (split
-    groups of `part` oscillators per workgroup when N > 1024)."""
+    groups of `part` oscillators per workgroup when N > 1024) in the given
+    coupling arithmetic."""
+    sp = "true" if coupling == "bf16x3" else "false"
     if N > 1024:
-        return f"kura_step_kernel<{(part or 1024) // 256}, true>"
-    return f"kura_step_kernel<{N // 256}, false>"
+        return f"kura_step_kernel<{(part or 1024) // 256}, true, {sp}>"
+    return f"kura_step_kernel<{N // 256}, false, {sp}>"
 
 
-def pmc_traffic(N, B, part=0):
+def pmc_traffic(N, B, part=0, coupling="f32"):
     """Bytes per launch of the step kernel from the committed rocprofv3 PMC
     passes (tools/rocprof_run.sh + tools/summarize_rocprof.py: FETCH_SIZE x2 +
     WRITE_SIZE, the same bench command).  PMC counters cannot be read from
@@ -231,7 +240,7 @@ def pmc_traffic(N, B, part=0):
         wl = d["bench_under_trace"]["config"]["workload"]
         if f"N={N} " not in wl or f"x {B} envs" not in wl:
             return None, None, None
-        k = d["kernels"][kernel_name(N, part)]
+        k = d["kernels"][kernel_name(N, part, coupling)]
         return (k["traffic_bytes_per_dispatch"], f"profiles/latest_rocprof.json ({d['source']}): FETCH_SIZE*2 + WRITE_SIZE",
                 k.get("effective_clock_ghz"))
     except (OSError, KeyError, ValueError):
@@ -262,7 +271,7 @@ def episode_bench(args, rank, world, local_rank):
         plist.append(p)
     t0 = time.perf_counter()
     env = vec.KuraVectorEnv(plist, device=local_rank, reward_func=args.reward, w0_seed=10_000_000 + args.seed + rank * B,
-                            episode_metrics=args.episode_metrics, profile=True)
+                            episode_metrics=args.episode_metrics, profile=True, coupling=args.coupling)
     setup_s = time.perf_counter() - t0
     dev = env.device
     env.reset()
@@ -415,6 +424,7 @@ def main(argv=None):
     sim.set_spectral(ctab, stab)
     t_setup = time.perf_counter() - t_setup
     B, N = cfg.n_envs, cfg.n_osc
+    coupling = sim_mod.abi.coupling_of(cfg)   # the arithmetic the handle runs
 
     th = torch.from_numpy(theta0).to(dev)
     torch.cuda.synchronize()
@@ -471,12 +481,18 @@ def main(argv=None):
         value = world * B * args.steps / el_max
         avg_kernel_s = float(np.mean(kern_ms)) / 1e3
         flop_per_launch = useful_rhs * 4.0 * N * N   # 2 length-N dot products per oscillator per sweep
-        achieved_tf = flop_per_launch / avg_kernel_s / 1e12
+        achieved_tf = flop_per_launch / avg_kernel_s / 1e12   # fp32-equivalent (algorithmic) TFLOP/s
+        # the roofline of the arithmetic the kernel executes: F32 products on the FP32 MFMA, or six bf16
+        # products per fp32 product on the BF16 MFMA (KURA_COUPLING_BF16X3, fp32 accumulation)
+        sp = coupling == "bf16x3"
+        exec_flop = flop_per_launch * (BF16X3_PRODUCTS if sp else 1)
+        exec_tf = exec_flop / avg_kernel_s / 1e12
+        peak_tf = PEAK_BF16_TFLOPS if sp else PEAK_FP32_TFLOPS
         # algorithmic HBM bytes per launch: per env theta r/w, omega, g_stim/g_rec (f64),
         # window r/w (f64 ring + f32 obs), outputs; alpha once per launch
         bytes_env = 8 * N + 4 * N + 8 * cfg.n_elec * N + 8 * max(cfg.n_rec, 0) * N + (8 + 8 + 4) * cfg.window + 64
         bytes_launch = B * bytes_env + 4 * N * N
-        traffic, traffic_src, clock_ghz = pmc_traffic(N, B, cfg.part_osc)
+        traffic, traffic_src, clock_ghz = pmc_traffic(N, B, cfg.part_osc, coupling)
         out = {
             "metric": (f"env steps/sec (whole node), N={N} osc x {world * B} envs over {world} GPUs" if args.global_envs
                        else f"env steps/sec (whole node), N={N} osc x {B} envs per GPU"),
@@ -491,27 +507,36 @@ def main(argv=None):
             "higher_is_better": True,
             "scaling": "strong" if args.global_envs else "weak",
             "vs_baseline": None,
-            "dtype": "f32",
+            "dtype": "f32 (bf16x3-split products, f32 accumulate)" if sp else "f32",
             "data": "synthetic (seeded reference-sampler natural frequencies, N(pi,0.6) phases, U(-1,1) actions)",
             "config": {"workload": f"{args.config} reference step(), N={N} oscillators x {B} envs per GPU, "
                                    f"adaptive Dopri5 rtol=atol=1e-5, W={cfg.window}, reward={args.reward}"
-                                   + (", per-env K~U(0.3,0.8)" if args.random_k else ", K=0.52"),
+                                   + (", per-env K~U(0.3,0.8)" if args.random_k else ", K=0.52")
+                                   + f", coupling={coupling}",
                        "global_envs": world * B, "parallelism": f"env-shard x{world} (no collectives)"}
                       | ({"part_osc": cfg.part_osc or 1024} if N > 1024 else {}),
-            "roofline": {"bound": "mfma", "achieved": achieved_tf, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
-                         "frac": achieved_tf / PEAK_FP32_TFLOPS, "traffic": traffic,
+            "roofline": {"bound": "mfma_bf16" if sp else "mfma", "achieved": exec_tf, "peak": peak_tf,
+                         "unit": "TFLOP/s", "frac": exec_tf / peak_tf, "traffic": traffic,
                          "traffic_source": traffic_src,
-                         "kernel": kernel_name(N, cfg.part_osc), "avg_kernel_ms": avg_kernel_s * 1e3,
-                         "flop_per_launch": flop_per_launch, "useful_rhs_per_launch": useful_rhs,
+                         "kernel": kernel_name(N, cfg.part_osc, coupling), "avg_kernel_ms": avg_kernel_s * 1e3,
+                         "flop_per_launch": exec_flop,
+                         "flop_basis": (f"executed bf16 MFMA FLOP: {BF16X3_PRODUCTS} products x 4N^2 per useful RHS sweep"
+                                        if sp else "4N^2 fp32 MFMA FLOP per useful RHS sweep"),
+                         "useful_rhs_per_launch": useful_rhs,
                          "hbm_alg_bytes_per_launch": bytes_launch,
                          "hbm_alg_gbs": bytes_launch / avg_kernel_s / 1e9},
-            "extra": {"rhs_sweeps_per_env_step": useful_rhs / B, "dopri_steps_attempted": steps_attempted,
+            "extra": {"coupling": coupling,
+                      "fp32_equivalent_tflops": achieved_tf,
+                      "fp32_equivalent_frac_of_fp32_peak": achieved_tf / PEAK_FP32_TFLOPS,
+                      "rhs_sweeps_per_env_step": useful_rhs / B, "dopri_steps_attempted": steps_attempted,
                       "rejected": rejected, "lockstep_efficiency": lockstep_eff,
-                      "executed_frac": (16.0 * wg_sweeps * 4.0 * N * N / avg_kernel_s / 1e12) / PEAK_FP32_TFLOPS, "phase_sweeps_per_s": world * useful_rhs / avg_kernel_s,
+                      "executed_frac": ((16.0 * wg_sweeps * 4.0 * N * N * (BF16X3_PRODUCTS if sp else 1))
+                                        / avg_kernel_s / 1e12) / peak_tf,
+                      "phase_sweeps_per_s": world * useful_rhs / avg_kernel_s,
                       # the chip holds its clock below 2.4 GHz under this kernel (DVFS): effective clock from the
                       # committed GRBM_GUI_ACTIVE pass (tools/rocprof_run.sh) and the FP32 MFMA peak at that clock
                       "effective_clock_ghz": clock_ghz,
-                      "frac_of_peak_at_effective_clock": (achieved_tf / (PEAK_FP32_TFLOPS * clock_ghz / 2.4)
+                      "frac_of_peak_at_effective_clock": (exec_tf / (peak_tf * clock_ghz / 2.4)
                                                           if clock_ghz else None),
                       "reset_ms": t_reset * 1e3, "reset_rhs_max": int(reset_stats[0]),
                       "host_setup_s": t_setup},

@@ -5,7 +5,7 @@ Import with ``importlib.import_module("dbs-gym_amd")`` (the directory name is
 not a Python identifier).  Numerics live in csrc/libkura.so (HIP, gfx950).
 """
 from . import abi, configs, model_setup, spectral  # noqa: F401
-from .abi import load_library  # noqa: F401
+from .abi import coupling_of, load_library  # noqa: F401
 from .configs import reference_params, synthetic_params  # noqa: F401
 from .batch import EnvHost, build_batch, fill_driver_arrays, fill_driver_arrays_batch, reset_arrays, reset_draws_batch  # noqa: F401
 

@@ -42,6 +42,21 @@ REWARD_KINDS = {
     "temp_const_action": KURA_R_TEMP_CONST,
     "bbpow_threth_action": KURA_R_BBPOW_THR,
 }
+# coupling arithmetic (kura.h KURA_COUPLING_*): "auto" = bf16x3 for N <= 1024, f32 above
+KURA_COUPLING_AUTO = 0
+KURA_COUPLING_F32 = 1
+KURA_COUPLING_BF16X3 = 2
+COUPLINGS = {"auto": KURA_COUPLING_AUTO, "f32": KURA_COUPLING_F32, "bf16x3": KURA_COUPLING_BF16X3}
+
+
+def coupling_of(cfg) -> str:
+    """The arithmetic a config resolves to (kura.h kura_coupling_of)."""
+    c = int(cfg.coupling)
+    if c == KURA_COUPLING_AUTO:
+        c = KURA_COUPLING_BF16X3 if cfg.n_osc <= 1024 else KURA_COUPLING_F32
+    return {KURA_COUPLING_F32: "f32", KURA_COUPLING_BF16X3: "bf16x3"}[c]
+
+
 # recording_kernel names (environment/env.py:333-338)
 REC_KERNELS = {"naive": KURA_REC_NAIVE, "gaussian": KURA_REC_GAUSSIAN}
 
@@ -71,7 +86,8 @@ class KuraConfig(ctypes.Structure):
         ("padlen", c_int32),
         ("episode_cap", c_int32),
         ("part_osc", c_int32),
-        ("reserved_i", c_int32 * 2),
+        ("coupling", c_int32),
+        ("reserved_i", c_int32 * 1),
         ("dt", c_double),
         ("width", c_double),
         ("pause", c_double),
@@ -95,6 +111,7 @@ class KuraConfig(ctypes.Structure):
 # exported by the KURA_DEBUG build (libkura_debug.so) only
 _DEBUG_SYMBOLS = {
     "kura_debug_read_workspace": (c_int, [c_void_p, c_void_p, c_int64]),
+    "kura_debug_gemm_dump": (c_int, [c_void_p, c_void_p, c_int]),
 }
 
 _SYMBOLS = {
@@ -128,6 +145,7 @@ _SYMBOLS = {
     "kura_get_stamps": (c_int, [c_void_p, c_void_p]),
     "kura_selftest_math": (c_int, [c_void_p, c_void_p, c_void_p, c_int]),
     "kura_selftest_gemm": (c_int, [c_void_p, c_void_p, c_void_p, c_int]),
+    "kura_selftest_coupling": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int]),
 }
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
@@ -200,5 +218,6 @@ __all__ = [
     "KURA_F_MAX_STEPS", "KURA_F_NONFINITE", "KURA_F_GRID", "KURA_F_BARRIER",
     "KURA_ABI_VERSION", "KURA_S_MAX", "KURA_MAX_BINS", "REWARD_KINDS", "REC_KERNELS",
     "KURA_REC_NAIVE", "KURA_REC_GAUSSIAN", "KURA_R_BBPOW", "KURA_R_TEMP_CONST", "KURA_R_BBPOW_THR",
+    "KURA_COUPLING_AUTO", "KURA_COUPLING_F32", "KURA_COUPLING_BF16X3", "COUPLINGS", "coupling_of",
     "c_int64", "c_uint8",
 ]

@@ -99,6 +99,8 @@ struct DevParams {
     int* ep_len;            // [B] samples appended since the env's last reset
     int* eflags;            // [B] per-env failure bits of the last launch (KURA_F_*, kura.h), 0 = ok
     float* rows;            // optional [B][KURA_S_MAX+1][N]: every saved row of a step (sol_state_, env.py:430,440)
+    float* gemm_dump;       // KURA_DEBUG builds: [sweep][2][32][N] operand and coupling sums of workgroup 0
+    int gemm_dump_n;        // ... sweeps to keep (kura_debug_gemm_dump)
 };
 
 // Device code reads DevParams where the dispatch put it: in the kernarg
@@ -228,15 +230,15 @@ __device__ __forceinline__ T* uniform_ptr(T* ptr) {
 }
 
 
-#ifdef KURA_SPLIT_GEMM
-// EXPERIMENT (built only as libkura_split.so for a
-// same-box timing A/B -- the oracle does not model it, so no parity test
-// runs it): the coupling from three-way bf16 splits on
-// v_mfma_f32_32x32x16_bf16, six part products per 16-deep k-block.  alpha
-// arrives pre-split (kura_set_coupling under the same macro): per column
-// tile jt, k-block b and part p, lane l holds 8 bf16 at k = 16b + 8(i/4) +
-// 2(i%4) + l/32 -- the k order of the fp32 operand image, so the sin/cos
-// rows are split from the same two float4 reads.
+// KURA_COUPLING_BF16X3 (kura.h): the coupling from
+// three-way bf16 splits on v_mfma_f32_32x32x16_bf16, six part products per
+// 16-deep k-block in the order x1a1, x1a2, x2a1, x1a3, x2a2, x3a1 (the oracle
+// restates the MFMA's accumulation exactly: oracle_split_gemm_rows, pinned by
+// tests/test_mfma_bf16_model.py and tests/test_gpu_split_gemm.py).  alpha
+// arrives pre-split (split_alpha, kura_capi.inc): per column tile jt, k-block
+// b and part p, lane l holds 8 bf16 at k = 16b + 8(i/4) + 2(i%4) + l/32 -- the
+// k order of the fp32 operand image, so the sin/cos rows are split from the
+// same two float4 reads of the LDS operand.
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 __device__ __forceinline__ void split_bf16x3(floatx4 lo, floatx4 hi, bf16x8& h1, bf16x8& h2, bf16x8& h3) {
 #pragma unroll
@@ -252,8 +254,8 @@ __device__ __forceinline__ void split_bf16x3(floatx4 lo, floatx4 hi, bf16x8& h1,
 }
 
 template <int TPW>
-__device__ __forceinline__ void coupling_gemm(const float* __restrict__ Xs, const float* __restrict__ alpha_sw,
-                                              floatx16 (&acc)[TPW], unsigned long long* dbg = nullptr) {
+__device__ __forceinline__ void coupling_gemm_bf16x3(const float* __restrict__ Xs, const float* __restrict__ alpha_sw,
+                                                     floatx16 (&acc)[TPW], unsigned long long* dbg = nullptr) {
     (void)dbg;
     constexpr int N = TPW * 32 * NWAVES;
     constexpr int NB = N / 16;
@@ -270,6 +272,7 @@ __device__ __forceinline__ void coupling_gemm(const float* __restrict__ Xs, cons
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
         (void*)((const char*)au + (size_t)wave * TPW * TSTRIDE), 0, TPW * TSTRIDE, 0x00020000);
     auto ld = [&](int t, int b, int p) -> bf16x8 {
+        KDBG_CHECK(dbg, b >= 0 && b < NB && ((b * 3 + p) * 64 + lane) * 16 + t * TSTRIDE + 16 <= TPW * TSTRIDE);
         return __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rs, ((b * 3 + p) * 64 + lane) * 16,
                                                                                  t * TSTRIDE, 0));
     };
@@ -302,11 +305,12 @@ __device__ __forceinline__ void coupling_gemm(const float* __restrict__ Xs, cons
         __builtin_amdgcn_sched_barrier(0);
     }
 }
-#else
-// wave w owns column tiles w*TPW .. w*TPW+TPW-1
+
+// KURA_COUPLING_F32: exact fp32, the k-ordered fmaf chain of
+// v_mfma_f32_32x32x2_f32.  Wave w owns column tiles w*TPW .. w*TPW+TPW-1.
 template <int TPW>
-__device__ __forceinline__ void coupling_gemm(const float* __restrict__ Xs, const float* __restrict__ alpha_sw,
-                                              floatx16 (&acc)[TPW], unsigned long long* dbg = nullptr) {
+__device__ __forceinline__ void coupling_gemm_f32(const float* __restrict__ Xs, const float* __restrict__ alpha_sw,
+                                                  floatx16 (&acc)[TPW], unsigned long long* dbg = nullptr) {
     (void)dbg;  // KURA_DEBUG: bounds flag target
     constexpr int N = TPW * 32 * NWAVES;
     constexpr int NK8 = N / 8;
@@ -372,7 +376,16 @@ __device__ __forceinline__ void coupling_gemm(const float* __restrict__ Xs, cons
         __builtin_amdgcn_sched_barrier(0);
     }
 }
-#endif  // KURA_SPLIT_GEMM
+
+// The coupling GEMM of a handle's arithmetic (SP: KURA_COUPLING_BF16X3).
+template <int TPW, bool SP>
+__device__ __forceinline__ void coupling_gemm(const float* __restrict__ Xs, const float* __restrict__ alpha_sw,
+                                              floatx16 (&acc)[TPW], unsigned long long* dbg = nullptr) {
+    if constexpr (SP)
+        coupling_gemm_bf16x3<TPW>(Xs, alpha_sw, acc, dbg);
+    else
+        coupling_gemm_f32<TPW>(Xs, alpha_sw, acc, dbg);
+}
 
 // Workgroup barrier that orders LDS only.  Inside a solve every workspace
 // record (R) is written and read back by the same lane (MFMA-layout
@@ -1621,13 +1634,14 @@ __device__ __forceinline__ int post_step(DevParamsK& __restrict__ p, Slot& ws, i
 #else
 #define KURA_SOLVE_ATTR __noinline__
 #endif
-template <int TPW, bool XL>
+template <int TPW, bool XL, bool SP>
 __device__ KURA_SOLVE_ATTR void solve_wg(DevParamsK& __restrict__ pin, float* Xs, int env_base, bool to_ring, bool pulse_on,
                          long long* rhs_count, Part& pt) {
     // (the kernarg segment through the VGPR-passed pointer: vector loads.
     // Made wave-uniform -- scalar loads, which share lgkmcnt with the LDS
     // traffic -- the step was 1.5 % slower in the same-box A/B,
     // profiles/r04_solver_ab.txt)
+    static_assert(!(XL && SP), "split env groups run the F32 coupling");
     DevParamsK& __restrict__ p = pin;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, tid = threadIdx.x;
     constexpr int N = TPW * 256;            // oscillators owned by this workgroup
@@ -1677,9 +1691,19 @@ __device__ KURA_SOLVE_ATTR void solve_wg(DevParamsK& __restrict__ pin, float* Xs
             coupling_gemm_xl<TPW>(xgrp, p.alpha_sw, Xs, NG, col0, acc STAMP_ARGS);
         } else {
 #ifdef KURA_DEBUG
-            coupling_gemm<TPW>(Xs, p.alpha_sw, acc, uniform_ptr(p.stats));
+            coupling_gemm<TPW, SP>(Xs, p.alpha_sw, acc, uniform_ptr(p.stats));
+            if (p.gemm_dump && blockIdx.x == 0 && nrhs < p.gemm_dump_n) {   // the sweep's operand and sums
+                float* d = p.gemm_dump + (size_t)nrhs * 2 * 32 * N;
+                for (int idx = tid; idx < 32 * N; idx += NTHREADS) d[idx] = Xs[xs_idx(idx / N, idx % N)];
+#pragma unroll
+                for (int t = 0; t < TPW; ++t)
+#pragma unroll
+                    for (int q = 0; q < 16; ++q)
+                        d[32 * N + (size_t)((q & 3) + 8 * (q >> 2) + 4 * (lane >> 5)) * N + 32 * (wave * TPW + t) +
+                          (lane & 31)] = acc[t][q];
+            }
 #else
-            coupling_gemm<TPW>(Xs, p.alpha_sw, acc);
+            coupling_gemm<TPW, SP>(Xs, p.alpha_sw, acc);
 #endif
         }
         STAMP(2);
@@ -1863,8 +1887,10 @@ __device__ __forceinline__ void r2_dot_multi(DevParamsK& __restrict__ p, const W
 // (and kura_set_state / kura_set_spec) forms Y directly (spec_init, R64
 // order); the oracle keeps the same accumulators with the same operations
 // (oracle/kura_oracle.c spec_update), so the reward stays bit-exact, and it
-// agrees with the direct DFT to float64 rounding (~1e-14 relative over an
-// episode, tests/test_oracle_props.py).
+// agrees with the direct DFT to float64 rounding: over a whole 5555-step
+// episode 2.2e-14 relative on the band power and 8.6e-15 of sum|x| on Y_k
+// (tests/test_r2_functional.py::test_accumulators_hold_over_a_whole_episode,
+// bound 1e-12).
 
 // whole wave: Y of env `env` from its ring (positions 0..W-1), R64 dots
 __device__ __forceinline__ void spec_init(DevParamsK& __restrict__ p, int env) {
@@ -1969,7 +1995,7 @@ __device__ __forceinline__ int launch_flags(DevParamsK& p, bool xl) {
     return (int)(v & KURA_F_BARRIER);
 }
 
-template <int TPW, bool XL>
+template <int TPW, bool XL, bool SP>
 __device__ __forceinline__ void step_pair(DevParamsK& p, Part& pt, float* Xs, const float* __restrict__ action,
                                           float* __restrict__ obs, double* __restrict__ reward,
                                           uint8_t* __restrict__ done, float* __restrict__ lfp_true,
@@ -2045,7 +2071,7 @@ __device__ __forceinline__ void step_pair(DevParamsK& p, Part& pt, float* Xs, co
             }
             __syncthreads();
         }
-        solve_wg<TPW, XL>(p, Xs, env_base, false, ph == 0, &rhs, pt);
+        solve_wg<TPW, XL, SP>(p, Xs, env_base, false, ph == 0, &rhs, pt);
     }
     STAMP_DECL  // diagnostic build: the tail's phases in slots 20-22
     __syncthreads();
@@ -2167,15 +2193,15 @@ __device__ __forceinline__ void step_pair(DevParamsK& p, Part& pt, float* Xs, co
 // wrongly -- deterministic, gone at -O3 with this call boundary, present at
 // -O2 as well (tools/parity_probe.py, profiles/r02_part256_probe.txt); the
 // GPU parity suite covers every instantiation.
-template <int TPW, bool XL>
+template <int TPW, bool XL, bool SP>
 __device__ __noinline__ void step_pair_call(DevParamsK& pin, Part& pt, float* Xs, const float* __restrict__ action,
                                             float* __restrict__ obs, double* __restrict__ reward,
                                             uint8_t* __restrict__ done, float* __restrict__ lfp_true,
                                             double* __restrict__ lfp_rec, int* __restrict__ nsamp) {
-    step_pair<TPW, XL>(pin, pt, Xs, action, obs, reward, done, lfp_true, lfp_rec, nsamp);
+    step_pair<TPW, XL, SP>(pin, pt, Xs, action, obs, reward, done, lfp_true, lfp_rec, nsamp);
 }
 
-template <int TPW, bool XL>
+template <int TPW, bool XL, bool SP>
 __global__ __launch_bounds__(NTHREADS) void kura_step_kernel(DevParams p_kernarg, const float* __restrict__ action,
                                                              float* __restrict__ obs, double* __restrict__ reward,
                                                              uint8_t* __restrict__ done, float* __restrict__ lfp_true,
@@ -2187,16 +2213,16 @@ __global__ __launch_bounds__(NTHREADS) void kura_step_kernel(DevParams p_kernarg
 #pragma unroll 1
         for (int pair = blockIdx.x; pair < p.npairs; pair += gridDim.x) {
             Part pt = make_part(p, pair);
-            step_pair_call<TPW, XL>(p, pt, Xs, action, obs, reward, done, lfp_true, lfp_rec, nsamp);
+            step_pair_call<TPW, XL, SP>(p, pt, Xs, action, obs, reward, done, lfp_true, lfp_rec, nsamp);
         }
     } else {
         Part pt = make_part(p, blockIdx.x);
-        step_pair<TPW, XL>(p, pt, Xs, action, obs, reward, done, lfp_true, lfp_rec, nsamp);
+        step_pair<TPW, XL, SP>(p, pt, Xs, action, obs, reward, done, lfp_true, lfp_rec, nsamp);
     }
 }
 
 // ----------------------------------------------------------- reset kernel --
-template <int TPW, bool XL>
+template <int TPW, bool XL, bool SP>
 __device__ __forceinline__ void reset_pair(DevParamsK& p, Part& pt, float* Xs, const uint8_t* __restrict__ mask,
                                            const float* __restrict__ theta0, float* __restrict__ obs) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, tid = threadIdx.x;
@@ -2221,7 +2247,7 @@ __device__ __forceinline__ void reset_pair(DevParamsK& p, Part& pt, float* Xs, c
     }
     __syncthreads();
     long long rhs = 0;
-    solve_wg<TPW, XL>(p, Xs, env_base, true, false, &rhs, pt);
+    solve_wg<TPW, XL, SP>(p, Xs, env_base, true, false, &rhs, pt);
     __syncthreads();  // ring rows written by thread e are read by every lane below
 #pragma unroll 1
     for (int ee = 0; ee < ((!XL || pt.part == 0) ? ENVS_PER_WAVE : 0); ++ee) {
@@ -2251,7 +2277,7 @@ __global__ __launch_bounds__(64) void kura_spec_init_kernel(DevParams p_kernarg)
     if ((int)blockIdx.x < p.B) spec_init(p, blockIdx.x);
 }
 
-template <int TPW, bool XL>
+template <int TPW, bool XL, bool SP>
 __global__ __launch_bounds__(NTHREADS) void kura_reset_kernel(DevParams p_kernarg, const uint8_t* __restrict__ mask,
                                                               const float* __restrict__ theta0,
                                                               float* __restrict__ obs) {
@@ -2262,11 +2288,11 @@ __global__ __launch_bounds__(NTHREADS) void kura_reset_kernel(DevParams p_kernar
 #pragma unroll 1
         for (int pair = blockIdx.x; pair < p.npairs; pair += gridDim.x) {
             Part pt = make_part(p, pair);
-            reset_pair<TPW, XL>(p, pt, Xs, mask, theta0, obs);
+            reset_pair<TPW, XL, SP>(p, pt, Xs, mask, theta0, obs);
         }
     } else {
         Part pt = make_part(p, blockIdx.x);
-        reset_pair<TPW, XL>(p, pt, Xs, mask, theta0, obs);
+        reset_pair<TPW, XL, SP>(p, pt, Xs, mask, theta0, obs);
     }
 }
 
@@ -2364,7 +2390,7 @@ __global__ void kura_selftest_math_kernel(const float* x, const float* y, float*
 }
 
 // One 32-row coupling GEMM through the production GEMM path.
-template <int TPW>
+template <int TPW, bool SP>
 __global__ __launch_bounds__(NTHREADS) void kura_selftest_gemm_kernel(const float* X, const float* alpha_sw,
                                                                        float* Y, int N) {
     extern __shared__ float Xs[];
@@ -2374,7 +2400,7 @@ __global__ __launch_bounds__(NTHREADS) void kura_selftest_gemm_kernel(const floa
     }
     __syncthreads();
     floatx16 acc[TPW];
-    coupling_gemm<TPW>(Xs, alpha_sw, acc);
+    coupling_gemm<TPW, SP>(Xs, alpha_sw, acc);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
     for (int t = 0; t < TPW; ++t)

@@ -72,10 +72,11 @@ def protocol_draws(name: str, n_episodes: int, n_envs: int = 5, seed: int = 228,
 
 
 def run_protocol(name: str, actions=(0.0, 1.0), n_episodes: int = 5, n_envs: int = 5, seed: int = 228,
-                 device=0, psd_dt: float = 5e-4, beta=(12.5, 21.0), **overrides):
+                 device=0, psd_dt: float = 5e-4, beta=(12.5, 21.0), coupling: str = "auto", **overrides):
     """Runs the protocol on the GPU for every (action, env) pair as one batch
     and returns {"bbpow": [n_actions, n_envs], "reward": [n_actions, n_envs, n_episodes],
-    "lfp": list of per-env concatenated theta_mean signals}."""
+    "lfp": list of per-env concatenated theta_mean signals}.  coupling: the
+    coupling arithmetic (KuraVectorEnv / make_config)."""
     import torch
 
     from .vec_env import KuraVectorEnv
@@ -84,7 +85,7 @@ def run_protocol(name: str, actions=(0.0, 1.0), n_episodes: int = 5, n_envs: int
     A = len(actions)
     batch_params = [p for _ in actions for p in plist]
     env = KuraVectorEnv(batch_params, device=device, rand_seeds=[p["rand_seed"] for p in batch_params],
-                        autoreset=True)
+                        autoreset=True, coupling=coupling)
     # the reference's draws, in the reference's order; both action arms replay
     # the same ones (each arm is a separate run of the script)
     env.hosts = [ReplayHost(draws[k][1:]) for _ in actions for k in range(n_envs)]

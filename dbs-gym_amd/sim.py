@@ -33,10 +33,13 @@ def auto_part_osc(n_osc: int, n_envs: int, n_cu: int = 256) -> int:
 
 
 def make_config(params: dict, n_envs: int, reward_func: str | None = None, max_steps: int = 4096,
-                episode_cap: int = 0, part_osc: int = 0) -> KuraConfig:
+                episode_cap: int = 0, part_osc: int = 0, coupling: str = "auto") -> KuraConfig:
     """Build the C config from a reference params dict (env.py:277-338).
     part_osc: split-group part width for N > 1024 (0 = 1024; auto_part_osc
-    picks one that fills the GPU)."""
+    picks one that fills the GPU).  coupling: the arithmetic of the O(N^2)
+    coupling sums (kura.h KURA_COUPLING_*): "bf16x3" (three-way bf16 splits on
+    the bf16 MFMA, fp32 accumulation), "f32" (fmaf chain on the fp32 MFMA) or
+    "auto" (bf16x3 for N <= 1024, f32 above); results depend on it bit for bit."""
     p = params
     step_len = p["electrode_width"] + p["electrode_pause"]                      # env.py:294
     wind_len = step_len * p["observe_wind_counts"]                               # env.py:296
@@ -87,6 +90,15 @@ def make_config(params: dict, n_envs: int, reward_func: str | None = None, max_s
     if part_osc and (part_osc not in (256, 512, 1024) or c.n_osc % part_osc):
         raise ValueError(f"part_osc={part_osc}: expected 256, 512 or 1024 dividing num_oscillators={c.n_osc}")
     c.part_osc = int(part_osc)
+    if coupling not in abi.COUPLINGS:
+        raise ValueError(f"coupling={coupling!r}: expected one of {sorted(abi.COUPLINGS)}")
+    c.coupling = abi.COUPLINGS[coupling]
+    if abi.coupling_of(c) == "bf16x3" and c.n_osc > 1024:
+        raise NotImplementedError("coupling='bf16x3' with num_oscillators > 1024: split env groups run the "
+                                  "f32 coupling")
+    if W < KURA_S_MAX:   # kura_create: a step's samples never wrap the ring twice
+        raise ValueError(f"observation window of {W} samples: libkura needs at least {KURA_S_MAX} "
+                         "(observe_wind_counts * (electrode_width + electrode_pause) / verbose_dt)")
     return c
 
 

@@ -94,6 +94,9 @@ class KuraVectorEnv:
                 failed env is truncated and autoreset in the same call).
                 Either way a solver failure ends the episode as truncated, not
                 terminated.
+    coupling:   arithmetic of the O(N^2) coupling sums (kura.h
+                KURA_COUPLING_*, ``make_config``): "auto" (default; "bf16x3"
+                for N <= 1024, "f32" above), "bf16x3" or "f32".
     """
 
     metadata = {"render.modes": ["human"]}
@@ -102,7 +105,7 @@ class KuraVectorEnv:
                  w0_seed: int = 228, rand_seeds=None, autoreset: bool = True, max_steps: int = 4096,
                  episode_metrics: bool = False, psd_dt: float = 5e-4, beta_band=(12.5, 21.0),
                  on_failure: str = "raise", profile: bool = False, failure_check: str = "deferred",
-                 max_reset_failures: int = 3, autoreset_mode: str = "same_step"):
+                 max_reset_failures: int = 3, autoreset_mode: str = "same_step", coupling: str = "auto"):
         if autoreset_mode not in ("same_step", "next_step"):
             raise ValueError(f"autoreset_mode={autoreset_mode!r}: expected 'same_step' or 'next_step'")
         self.autoreset_mode = autoreset_mode
@@ -140,7 +143,8 @@ class KuraVectorEnv:
         self.hosts, shared = build_batch(plist)
         ep_steps = int(plist[0]["total_episode_len"] / (plist[0]["electrode_width"] + plist[0]["electrode_pause"]))
         self.cfg = make_config(plist[0], B, reward_func=plist[0]["reward_func"], max_steps=max_steps,
-                               episode_cap=(ep_steps + 1) * KURA_S_MAX if episode_metrics else 0)
+                               episode_cap=(ep_steps + 1) * KURA_S_MAX if episode_metrics else 0,
+                               coupling=coupling)
         self.episode_metrics = episode_metrics
         self.psd_dt, self.beta_band = psd_dt, tuple(beta_band)
         self.sim = KuraSim(self.cfg, device)
@@ -165,7 +169,9 @@ class KuraVectorEnv:
         # deferred failure flags: pinned host copies of the last step's and the
         # last autoreset's per-env flags, and the events that complete them
         self._pend = None          # (flags_pinned, event, reset_mask or None, reset_flags_pinned)
-        self._pend_discard = None  # next_step mode: envs whose step in that launch was discarded
+        self._pend_ignore = None   # envs whose step flags of the pending launch do not count (bool mask):
+                                   # next_step resets (step discarded) and envs reported truncated
+        self._trunc_next = None    # next_step + deferred: (env ids, last obs) to report truncated after the launch
         self._reset_fail_runs = np.zeros(B, np.int64)   # consecutive failed resets per env
         self._pending_gain = {}    # env -> float32(K/N) of a set_attr'd params_dict, applied at its next reset
         self._omega = np.zeros((B, self.N), np.float32)
@@ -223,7 +229,7 @@ class KuraVectorEnv:
         infos: dict = {}
         # deferred flags of the last step() (a failure there raises here in
         # "raise" mode, as the reference's failing diffeqsolve would have)
-        pre_failed, pre_flags, pre_rfail = self._take_pending()
+        pre_failed, pre_flags, pre_rfail, _ = self._take_pending()
         if self.on_failure == "raise" and (len(pre_failed) or len(pre_rfail)):
             self._act_on_failures(pre_failed, pre_flags, pre_rfail, {}, "kura_step (previous call)")
         if len(pre_failed):
@@ -233,6 +239,7 @@ class KuraVectorEnv:
         self._check_reset(None, infos)
         self.steps[:] = 0
         self._next_reset = None
+        self._trunc_next = None
         self._was_reset = True
         return obs.view(self.num_envs, 1, self.W).clone(), infos
 
@@ -242,24 +249,40 @@ class KuraVectorEnv:
 
     def _take_pending(self):
         """The deferred flags of the previous step (and of its autoreset):
-        (failed env ids, flags, failed reset ids).  Waits only for the copies,
-        which the previous launches completed long ago in a stepping loop."""
+        (failed env ids, flags, failed reset ids, ended), ``ended[i]``: the
+        episode of failed env i already ended in that call -- same_step mode:
+        it was autoreset there; next_step mode: it finished there and is reset
+        in this call -- so it needs its failure reported, not a reset
+        (ADVICE r04).  Waits only for the copies, which the previous launches
+        completed long ago in a stepping loop."""
         if self._pend is None:
-            return np.zeros(0, np.int64), np.zeros(0, np.int32), np.zeros(0, np.int64)
+            self._pend_ignore = None
+            return np.zeros(0, np.int64), np.zeros(0, np.int32), np.zeros(0, np.int64), np.zeros(0, bool)
         fl, ev, rmask, rfl = self._pend
         self._pend = None
         ev.synchronize()
         f = fl.numpy().copy()
-        if rmask is not None and self._pend_discard is not None:
-            f[self._pend_discard] = 0     # next_step mode: those envs' steps were discarded (reset instead)
-        self._pend_discard = None
+        if self._pend_ignore is not None:
+            f[self._pend_ignore] = 0      # steps discarded in that launch (reset instead, or already reported)
+        self._pend_ignore = None
         idx = np.nonzero(f)[0]
+        ended = np.zeros(len(idx), bool)
+        if rmask is not None and self.autoreset_mode == "same_step":
+            ended |= rmask[idx]
+        if self._next_reset is not None:
+            ended |= self._next_reset[idx]
         ridx = np.zeros(0, np.int64)
         if rmask is not None:
             rf = np.where(rmask, rfl.numpy(), 0)
             ridx = np.nonzero(rf)[0]
             self._reset_fail_runs[rmask & (rf == 0)] = 0      # those resets succeeded
-        return idx, f[idx], ridx
+        return idx, f[idx], ridx, ended
+
+    def _ignore_flags(self, envs):
+        """The pending launch's step flags of these envs do not count."""
+        m = np.zeros(self.num_envs, bool)
+        m[np.asarray(envs, np.int64)] = True
+        self._pend_ignore = m if self._pend_ignore is None else (self._pend_ignore | m)
 
     def _stash_flags(self, reset_mask=None):
         """Start the asynchronous copy of the last launch's flags (step, or the
@@ -287,9 +310,11 @@ class KuraVectorEnv:
                             device=self.device, dtype=torch.float32).reshape(self.num_envs, self.n_elec)
         infos: dict = {}
         # the previous step's deferred failures (and its autoreset's), before this launch
-        pre_failed, pre_flags, pre_rfail = self._take_pending()
+        pre_failed, pre_flags, pre_rfail, pre_ended = self._take_pending()
         if len(pre_failed) or len(pre_rfail):
-            self._act_on_failures(pre_failed, pre_flags, pre_rfail, infos, "kura_step (previous call)")
+            self._act_on_failures(pre_failed, pre_flags, pre_rfail, infos, "kura_step (previous call)", pre_ended)
+        trunc = self._trunc_next   # next_step mode: failed episodes to end in this call's outputs
+        self._trunc_next = None
         lo, hi = self.cfg.dbs_lo, self.cfg.dbs_hi
         x, y = self.cfg.act_lo, self.cfg.act_hi
         self.u = lo + ((hi - lo) * (a.double() - x)) / (y - x)      # env.py:389-393 (for callers)
@@ -311,6 +336,21 @@ class KuraVectorEnv:
         truncated = torch.zeros_like(terminated)
         if "reset_before_step_ids" in infos:
             truncated[torch.as_tensor(infos["reset_before_step_ids"], device=self.device)] = True
+        if trunc is not None:
+            # next_step mode (gymnasium NEXT_STEP): the failed episode ends in this
+            # call with its last observation, truncated, reward 0; its step in this
+            # launch (from an undefined state) is discarded and the next call
+            # resets it, as for an episode that ends on its own
+            tids, last_obs = trunc
+            d = torch.as_tensor(tids, device=self.device)
+            obs[d] = last_obs
+            rew[d] = 0.0
+            truncated[d] = True
+            terminated[d] = False
+            term_host = term_host.copy()
+            term_host[tids] = True
+            if self.failure_check != "eager":
+                self._ignore_flags(tids)
         if self.failure_check == "eager":
             failed, fflags = self._failures_now()         # synchronises: the step's outputs are ready
             if nxt is not None:                           # discarded steps do not fail an episode
@@ -356,7 +396,7 @@ class KuraVectorEnv:
                 self._check_reset(mask)
             else:
                 self._stash_flags(reset_mask=mask.numpy().astype(bool))
-                self._pend_discard = mask.numpy().astype(bool)
+                self._ignore_flags(nxt)
             if self.profile:
                 torch.cuda.synchronize(self.device)
             tb.update(n_reset=len(nxt), host_draw_s=self._t_draw, upload_s=self._t_upload,
@@ -409,23 +449,37 @@ class KuraVectorEnv:
         self.steps[ridx] = 0
         self._check_reset(mask, infos)
 
-    def _act_on_failures(self, failed, fflags, rfailed, infos, what):
+    def _act_on_failures(self, failed, fflags, rfailed, infos, what, ended=None):
         """Deferred failures of the previous call: raise, or report them and
-        reset those envs now (before this step's launch)."""
+        end those episodes.  same_step mode: reset the envs now (before this
+        step's launch), their last observation in
+        ``infos["reset_before_step_observation"]``; next_step mode: this
+        call reports them truncated with their last observation and the next
+        call resets them (``_trunc_next``).  Envs whose episode already ended
+        in the previous call (``ended``: autoreset there, or queued for this
+        call's next_step reset) are only reported -- resetting them again
+        would take an extra draw from their RNG stream."""
         if self.on_failure == "raise":
             if len(failed):
                 raise KuraSolverError(what, failed.tolist(), fflags.tolist())
             raise KuraSolverError("kura_reset (autoreset of the previous call)", rfailed.tolist(),
                                   [0] * len(rfailed))
+        live = np.zeros(0, np.int64)
         if len(failed):
             infos["failed_env_ids"] = failed
             infos["failure_flags"] = fflags
+            live = failed if ended is None else failed[~np.asarray(ended, bool)]
+        if len(live) and self.autoreset_mode == "next_step":
+            # the last observation, before this call's launch overwrites the buffer
+            self._trunc_next = (live, self.sim.obs[torch.as_tensor(live, device=self.device)].clone())
+            live = np.zeros(0, np.int64)
+        elif len(live):
             # the failed episodes end here (truncated): their last observation,
             # before the reset below overwrites the buffer
-            infos["reset_before_step_ids"] = failed
+            infos["reset_before_step_ids"] = live
             infos["reset_before_step_observation"] = \
-                self.sim.obs[torch.as_tensor(failed, device=self.device)].clone().view(-1, 1, self.W)
-        redo = np.union1d(failed, rfailed).astype(np.int64)
+                self.sim.obs[torch.as_tensor(live, device=self.device)].clone().view(-1, 1, self.W)
+        redo = np.union1d(live, rfailed).astype(np.int64)
         if len(rfailed):
             self._reset_fail_runs[rfailed] += 1
             over = rfailed[self._reset_fail_runs[rfailed] > self.max_reset_failures]
@@ -589,7 +643,7 @@ class KuraVectorEnv:
     def close(self):
         """Releases the handle; in "raise" mode a failure of the last step()
         that was not yet read (deferred flags) is raised after the release."""
-        pre_failed, pre_flags, pre_rfail = self._take_pending() if self._pend is not None else ([], [], [])
+        pre_failed, pre_flags, pre_rfail, _ = self._take_pending() if self._pend is not None else ([], [], [], [])
         self.sim.close()
         if self.on_failure == "raise" and (len(pre_failed) or len(pre_rfail)):
             self._act_on_failures(np.asarray(pre_failed), np.asarray(pre_flags), np.asarray(pre_rfail), {},

@@ -11,7 +11,8 @@
  * kura_reset never allocate device memory (kura_create does it once); the
  * episode-metric calls grow a per-handle scratch on demand and kura_reward_n
  * builds (synchronously, once per window length) the R2 filter functional of
- * that length.  Errors
+ * that length, keeping those of the 4 most recently used lengths (a fifth
+ * length synchronises the device and frees the least recently used).  Errors
  * never throw across the ABI: every
  * call returns 0 on success or a negative KURA_E* code, and
  * kura_last_error() returns a thread-local message.
@@ -82,6 +83,22 @@ enum {
 };
 
 enum { KURA_REC_NAIVE = 0, KURA_REC_GAUSSIAN = 1 };             /* env.py:333-338 */
+
+/* Coupling arithmetic (KuraConfig.coupling).  Both are exact, deterministic
+ * restatements of the reference's fp32 sum (env.py:252-256, JAX x64 off) with
+ * different last-bit rounding; both agree with the reference's own op
+ * sequence to <= 5e-7 absolute per RHS (tests/test_golden_reference.py):
+ *   F32     every product and sum in fp32: a k-ordered fmaf chain from +0
+ *           (v_mfma_f32_32x32x2_f32 computes exactly that);
+ *   BF16X3  each fp32 operand split into three bf16 parts (x = x1 + x2 + x3,
+ *           round-to-nearest-even, exact residuals), the six products
+ *           x1a1, x1a2, x2a1, x1a3, x2a2, x3a1 per 16-deep k-block on
+ *           v_mfma_f32_32x32x16_bf16 with fp32 accumulation (the oracle
+ *           restates that MFMA's accumulation exactly); ~1.4x the F32 rate;
+ *   AUTO    BF16X3 for n_osc <= 1024, F32 above (split env groups). */
+enum { KURA_COUPLING_AUTO = 0, KURA_COUPLING_F32 = 1, KURA_COUPLING_BF16X3 = 2 };
+/* kura_coupling_of(cfg), below: the arithmetic a config resolves to (the
+ * library and the oracle share it) */
 enum { KURA_R_BBPOW = 1, KURA_R_TEMP_CONST = 2, KURA_R_BBPOW_THR = 3 }; /* env.py:323-330 */
 
 typedef struct KuraConfig {
@@ -105,7 +122,11 @@ typedef struct KuraConfig {
                               (0 = 1024); smaller parts put more workgroups on the chip when the
                               handle has few envs.  It fixes the solver's reduction order (the
                               oracle follows it), so results depend on it bit for bit. */
-    int32_t reserved_i[2];
+    int32_t coupling;      /* KURA_COUPLING_*: the arithmetic of the O(N^2) coupling sums
+                              P = alpha.sin(theta), Q = alpha.cos(theta) of every RHS
+                              (env.py:252-256); results depend on it bit for bit, and the
+                              oracle follows it (kura_coupling_of) */
+    int32_t reserved_i[1];
     double dt;             /* verbose_dt: save-grid spacing (units) */
     double width;          /* electrode_width: stimulation ON interval */
     double pause;          /* electrode_pause: OFF interval */
@@ -121,6 +142,11 @@ typedef struct KuraConfig {
     float dt0;             /* diffeqsolve dt0 = 0.05, env.py:267 */
     float reserved_f[4];
 } KuraConfig;
+
+static inline int kura_coupling_of(const struct KuraConfig* c) {
+    if (c->coupling == KURA_COUPLING_AUTO) return c->n_osc <= 1024 ? KURA_COUPLING_BF16X3 : KURA_COUPLING_F32;
+    return c->coupling;
+}
 
 typedef struct KuraHandle KuraHandle;
 
@@ -228,6 +254,10 @@ int kura_set_spec(KuraHandle* h, const double* in);
  * B rounded up to 16; syncs) to the host -- used to compare kernel
  * generations record by record (tools/record_probe.py) */
 int kura_debug_read_workspace(KuraHandle* h, float* out, int64_t n);
+/* ... and keep the sin/cos operand and the coupling sums of the first n RHS
+ * sweeps of workgroup 0 (N <= 1024) in dev_buf ([n][2][32][N] float32, device;
+ * NULL stops) -- tools/coupling_dump_probe.py */
+int kura_debug_gemm_dump(KuraHandle* h, float* dev_buf, int n);
 #endif
 /* optional capture of every saved phase row of each kura_step: rows_dev
  * (device, B*(KURA_S_MAX+1)*N float32, or NULL to stop) receives, per env,
@@ -254,9 +284,11 @@ int kura_get_stats(KuraHandle* h, int64_t* out, int n);
  * the step path).  selftest_math writes 10 floats per element: sin, cos,
  * fmod2pi, inv_fifth_root(|y|), sqrt(|x|), x/y, f32(f64 x / f64 y),
  * ceil(x/0.05), and sin, cos of fmod(x, 2pi_f) (the RHS's folded reduction).  selftest_gemm runs the production MFMA coupling GEMM on one
- * 32 x N operand: Y[r][i] = sum_k X[r][k] * alpha[i][k]. */
+ * 32 x N operand: Y[r][i] = sum_k X[r][k] * alpha[i][k] (N in {256, 512, 1024}). */
 int kura_selftest_math(const float* x, const float* y, float* out, int n);
-int kura_selftest_gemm(const float* X, const float* alpha, float* Y, int N);
+int kura_selftest_gemm(const float* X, const float* alpha, float* Y, int N);   /* KURA_COUPLING_F32 */
+/* the same through the GEMM of a coupling arithmetic (KURA_COUPLING_*; AUTO = BF16X3 at these N) */
+int kura_selftest_coupling(const float* X, const float* alpha, float* Y, int N, int coupling);
 /* per-wave phase cycle counters of a -DKURA_STAMPS build ([8 waves][16]:
  * stage-input, barrier, GEMM, epilogue, barrier, post-step error pass, flag,
  * post-step decision, saves, FSAL, time advance, 5 spare; tools/phase_stamps.py);

@@ -84,6 +84,8 @@ class Oracle:
         self.N, self.B, self.W = cfg.n_osc, cfg.n_envs, cfg.window
         self._alpha = np.ascontiguousarray(alpha, np.float32)
         self._ctx = lib().oracle_create(ctypes.byref(cfg), self._alpha.ctypes.data)
+        if not self._ctx:
+            raise ValueError(f"oracle_create refused the config (coupling={cfg.coupling}, n_osc={cfg.n_osc})")
         B, N, W = self.B, self.N, self.W
         self.y = np.zeros((B, N), np.float32)
         self.t = np.zeros(B, np.float64)
@@ -102,8 +104,10 @@ class Oracle:
                       else np.zeros((self.B, nr, self.N), np.float64))
 
     def set_split(self, on=True):
-        """Model the KURA_SPLIT_GEMM build's coupling (three-way bf16 splits on
-        the bf16 MFMA) instead of the fp32 chain."""
+        """Override the config's coupling arithmetic (kura.h KURA_COUPLING_*):
+        on = KURA_COUPLING_BF16X3 (three-way bf16 splits on the bf16 MFMA's
+        exact accumulation), off = KURA_COUPLING_F32 (the fp32 fmaf chain).
+        The constructor already follows cfg.coupling (kura_coupling_of)."""
         rc = lib().oracle_set_split(self._ctx, int(bool(on)))
         if rc != 0:
             raise ValueError(f"oracle_set_split: rc={rc} (N <= 1024, N % 16 == 0)")

@@ -16,12 +16,14 @@ ev = importlib.import_module("dbs-gym_amd.evaluation")
 sim = importlib.import_module("dbs-gym_amd.sim")
 
 
-def oracle_protocol(name, n_episodes, actions=(0.0, 1.0), n_envs=5, psd_dt=5e-4, beta=(12.5, 21.0), **overrides):
-    """Returns bbpow [n_actions, n_envs] and the concatenated theta_mean signals."""
+def oracle_protocol(name, n_episodes, actions=(0.0, 1.0), n_envs=5, psd_dt=5e-4, beta=(12.5, 21.0), coupling="f32",
+                    **overrides):
+    """Returns bbpow [n_actions, n_envs] and the concatenated theta_mean signals
+    (coupling: KuraConfig.coupling of the run)."""
     from oracle import kura_eval
     plist, draws = ev.protocol_draws(name, n_episodes, n_envs, **overrides)
     B = len(actions) * n_envs
-    cfg = sim.make_config(plist[0], B, reward_func="bbpow_action")
+    cfg = sim.make_config(plist[0], B, reward_func="bbpow_action", coupling=coupling)
     _, shared = kura.build_batch([p for _ in actions for p in plist])
     o = ko.Oracle(cfg, shared["alpha"].astype(np.float32))
     o.set_gain(shared["gain"])

@@ -15,8 +15,10 @@ kura = importlib.import_module("dbs-gym_amd")
 from oracle import kura_oracle as ko  # noqa: E402
 
 
-def make_case(name="env0", n_osc=512, n_envs=4, reward="bbpow_action", seed=0, split="train", **overrides):
-    """Returns (cfg, alpha_f32, omega, g_stim, g_rec, theta0, ctab, stab, hosts)."""
+def make_case(name="env0", n_osc=512, n_envs=4, reward="bbpow_action", seed=0, split="train", coupling="auto",
+              **overrides):
+    """Returns (cfg, alpha_f32, omega, g_stim, g_rec, theta0, ctab, stab, hosts).
+    coupling: KuraConfig.coupling ("auto" = the product default)."""
     from importlib import import_module
     sim = import_module("dbs-gym_amd.sim")
     if n_osc == 512:
@@ -30,7 +32,7 @@ def make_case(name="env0", n_osc=512, n_envs=4, reward="bbpow_action", seed=0, s
         plist.append(kura.fill_driver_arrays(p, w0_seed=seed * 1000 + b))
     hosts, shared = kura.build_batch(plist)
     omega, g_stim, g_rec, theta0 = kura.reset_arrays(hosts)
-    cfg = sim.make_config(base, n_envs, reward_func=reward)
+    cfg = sim.make_config(base, n_envs, reward_func=reward, coupling=coupling)
     bins = kura.spectral.beta_bins(cfg.window, base["verbose_dt"])
     ctab, stab = kura.spectral.twiddles(cfg.window, bins)
     return cfg, shared["alpha"].astype(np.float32), omega, g_stim, g_rec, theta0, ctab, stab, hosts

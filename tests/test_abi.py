@@ -20,6 +20,7 @@ def declared_functions(debug=False):
     """Entry points declared by kura.h (debug=False: without the KURA_DEBUG-only block)."""
     src = open(HEADER).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    src = re.sub(r"static inline[^;{]*\{.*?\n\}", "", src, flags=re.S)   # header-only helpers (kura_coupling_of)
     if not debug:
         src = re.sub(r"#ifdef KURA_DEBUG.*?#endif", "", src, flags=re.S)
     return sorted(set(re.findall(r"\b(kura_[a-z_0-9]+)\s*\(", src)))
@@ -75,7 +76,8 @@ def test_config_struct_layout_matches_c():
 #define P(f) printf(#f " %zu\n", offsetof(KuraConfig, f));
 int main(void) {
   printf("sizeof %zu\n", sizeof(KuraConfig));
-  P(abi_version) P(n_osc) P(bins) P(padlen) P(dt) P(transient_len) P(dbs_hi) P(bw_b) P(bw_zi)
+  P(abi_version) P(n_osc) P(bins) P(padlen) P(part_osc) P(coupling) P(reserved_i) P(dt) P(transient_len) P(dbs_hi)
+  P(bw_b) P(bw_zi)
   P(rtol) P(kn) P(dt0) P(reserved_f)
   return 0;
 }

@@ -182,6 +182,22 @@ def test_gpu_reward_any_length(gpu, L):
 
 
 @pytest.mark.gpu
+def test_gpu_reward_r2_functional_cache_is_bounded(gpu):
+    """kura_reward_n keeps the R2 functionals of the 4 most recently
+    used window lengths; more lengths evict the least recently used (after a
+    device sync), and an evicted length is rebuilt -- every result stays the
+    oracle's."""
+    env = _venv(num_envs=1)
+    dt = float(G["rw_verbose_dt"][0])
+    x = G["rw_x_4680"]
+    lengths = [2340, 1000, 1500, 2000, 2500, 3000, 1000, 2340, 4680, 16, 1000]
+    for L in lengths:
+        got = float(env.reward_of(x[:L], [0.3], 2)[0].item())
+        assert got == _oracle_reward(2, x[:L], 0.3, dt), L
+    env.close()
+
+
+@pytest.mark.gpu
 def test_gpu_side_attributes(gpu):
     env = _venv()
     env.reset()

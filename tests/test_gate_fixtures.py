@@ -1,0 +1,45 @@
+"""The committed records of the product-arithmetic 1000-step gates
+(tests/golden/gate_*.npz, tests/golden/make_gate_fixtures.py) are the
+oracle's: a prefix of each scenario re-run live through the split-bf16 oracle
+on the CPU reproduces the record's reset state, reset observation and
+rewards bit for bit.  (The GPU side replays the whole record,
+tests/test_gpu_gates.py.)"""
+import os
+
+import numpy as np
+import pytest
+
+import gate_scenarios as gs
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+@pytest.mark.parametrize("scenario,steps", [("env0_r1", 2), ("env1_r2", 1), ("env2_r1_vec", 1)])
+def test_record_prefix_is_the_oracle(scenario, steps, monkeypatch):
+    R = np.load(os.path.join(GOLDEN, f"gate_{scenario}.npz"))
+    assert str(R["coupling"]) == "bf16x3"
+    monkeypatch.setattr(gs, "STEPS", steps)
+    monkeypatch.setattr(gs, "CHECK", ())
+    rec = gs.run_oracle_env2() if scenario == "env2_r1_vec" else gs.run_oracle_env01(scenario)
+    assert rec["reset_obs_sha1"].tobytes() == R["reset_obs_sha1"].tobytes()
+    for k in gs.STATE_KEYS:
+        np.testing.assert_array_equal(rec[f"reset_{k}"], R[f"reset_{k}"], err_msg=k)
+    assert rec["reset_ring_sha1"].tobytes() == R["reset_ring_sha1"].tobytes()
+    np.testing.assert_array_equal(rec["rewards"], R["rewards"][:steps])
+
+
+def test_records_hold_the_gate():
+    """Each record reaches step 1000 with a finite state, the env2 one through
+    three autoresets (reset step counters back at 0 at steps 300/600/900)."""
+    for name in gs.SCENARIOS:
+        R = np.load(os.path.join(GOLDEN, f"gate_{name}.npz"))
+        assert R["rewards"].shape == (gs.STEPS, gs.B)
+        assert np.all(np.isfinite(R["rewards"])) and np.all(np.isfinite(R["s1000_y"]))
+        if name == "env2_r1_vec":
+            assert R["s1000_t"].min() > 200.0 + 80.0   # the transient + 100 steps since the third reset
+            for r in (1, 2, 3):
+                assert np.all(R[f"r{r}_step"] == 0)
+            np.testing.assert_array_equal(R["s1000_step"], 100)
+        else:
+            assert R["s1000_t"].min() > 200.0 + 800.0   # the transient + 1000 steps of 0.80-0.90 units
+            np.testing.assert_array_equal(R["s1000_step"], 1000)

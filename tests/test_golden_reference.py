@@ -25,6 +25,11 @@ import pytest
 from helpers import ko, kura
 
 G = np.load(os.path.join(os.path.dirname(__file__), "golden", "reference_golden.npz"))
+# the product arithmetic's pins (tests/golden/make_golden_r05.py): the reference RHS on
+# more states (env1, the wavelet kernel, |y| up to 6e3, N=1024) and reset + 60 steps
+# of the reference plumbing with the bf16x3 solver
+G5 = np.load(os.path.join(os.path.dirname(__file__), "golden", "reference_r05.npz"))
+COUPLINGS = ("f32", "bf16x3")
 ms = importlib.import_module("dbs-gym_amd.model_setup")
 sim_mod = importlib.import_module("dbs-gym_amd.sim")
 
@@ -61,29 +66,51 @@ def test_conductances(tag, ec, rc, cm):
         assert (gs > 0).sum() == 511
 
 
-def _oracle_for(n=512, reward="bbpow_action", rec="naive", n_envs=1):
-    p = kura.reference_params("env0")
+def _oracle_for(n=512, reward="bbpow_action", rec="naive", n_envs=1, coupling="auto", alpha=None):
+    p = kura.reference_params("env0") if n == 512 else kura.synthetic_params("env0", n)
     p["recording_kernel"] = rec
-    cfg = sim_mod.make_config(p, n_envs, reward_func=reward)
-    alpha = ms.coupling_alpha(G["setup_env0_coords"]).astype(np.float32)
+    cfg = sim_mod.make_config(p, n_envs, reward_func=reward, coupling=coupling)
+    if alpha is None:
+        alpha = ms.coupling_alpha(G["setup_env0_coords"]).astype(np.float32)
     o = ko.Oracle(cfg, alpha)
     bins = kura.spectral.beta_bins(cfg.window, 0.05)
     o.set_spectral(*kura.spectral.twiddles(cfg.window, bins))
     return o, cfg
 
 
-def test_rhs_matches_reference_op_sequence():
+RHS_ATOL = 5e-7   # |f| ~ 5: 2 ulp; the reference's own fp32 rounding differs from either arithmetic
+
+
+@pytest.mark.parametrize("coupling", COUPLINGS)
+def test_rhs_matches_reference_op_sequence(coupling):
     """env.py:252-256 in fp32 (direct sin(theta_j - theta_i)) vs the oracle's
-    factorised fmaf form with the folded fmod/sincos reduction: same function,
-    different rounding.  Measured max |diff| 2.4e-7 (1 ulp at |f| ~ 4.8);
-    the pin is 5e-7 (VERDICT r03 weak #1)."""
-    o, _ = _oracle_for()
+    factorised form with the folded fmod/sincos reduction, in both coupling
+    arithmetics (kura.h KURA_COUPLING_*): same function, different rounding.
+    Measured max |diff| 2.4e-7 (f32) / 4.8e-7 (bf16x3) at |f| ~ 4.8; the pin
+    is 5e-7 (VERDICT r03 weak #1)."""
+    o, _ = _oracle_for(coupling=coupling)
     worst = 0.0
     for y, f_ref in zip(G["rhs_y"], G["rhs_f"]):
         f = o.rhs(y, G["rhs_w0"], G["rhs_pulse"])
-        np.testing.assert_allclose(f, f_ref, rtol=0, atol=5e-7)
+        np.testing.assert_allclose(f, f_ref, rtol=0, atol=RHS_ATOL)
         worst = max(worst, float(np.abs(f.astype(np.float64) - f_ref).max()))
     assert worst > 0.0      # the fixture really is the reference's own op sequence, not ours
+
+
+@pytest.mark.parametrize("coupling", COUPLINGS)
+@pytest.mark.parametrize("case", ["env0", "env1", "wavelet", "n1024"])
+def test_rhs_matches_reference_op_sequence_r05(coupling, case):
+    """The same pin on the reference's RHS for env0 with phases up to 6e3 rad,
+    env1's eval env (its locus, electrode and w0), the wavelet kernel (signed
+    alpha, utils.py:469-475) and N = 1024 on the BASELINE 16x8x8 grid
+    (tests/golden/make_golden_r05.py; VERDICT r04 next #1).  The worst case
+    is reported by tests/golden/make_golden_r05.py's companion note in
+    DESIGN.md."""
+    n = G5[f"rhs_{case}_y"].shape[1]
+    o, _ = _oracle_for(n=n, coupling=coupling, alpha=G5[f"rhs_{case}_alpha"])
+    for y, f_ref in zip(G5[f"rhs_{case}_y"], G5[f"rhs_{case}_f"]):
+        f = o.rhs(y, G5[f"rhs_{case}_w0"], G5[f"rhs_{case}_pulse"])
+        np.testing.assert_allclose(f, f_ref, rtol=0, atol=RHS_ATOL, err_msg=f"{case} {coupling}")
 
 
 def test_lfp_naive_and_distance():
@@ -151,12 +178,16 @@ def test_reset_draws_match_reference(tag, reward):
     np.testing.assert_allclose(g_rec, G[f"traj_{tag}_grec"], rtol=0, atol=4.5e-16)
 
 
+@pytest.mark.parametrize("coupling", COUPLINGS)
 @pytest.mark.parametrize("tag,reward", [("env0", "bbpow_action"), ("env1", "temp_const_action")])
-def test_trajectory_through_reference_plumbing(tag, reward):
+def test_trajectory_through_reference_plumbing(tag, reward, coupling):
     """reset + 60 steps of the reference SpatialKuramoto (its own step()/reset()
-    plumbing, this build's solver) vs oracle_reset/oracle_step."""
+    plumbing, this build's solver in the given coupling arithmetic:
+    reference_golden.npz for f32, reference_r05.npz for bf16x3) vs
+    oracle_reset/oracle_step."""
+    G = globals()["G"] if coupling == "f32" else G5
     p = _params_for(tag)
-    cfg = sim_mod.make_config(p, 1, reward_func=reward)
+    cfg = sim_mod.make_config(p, 1, reward_func=reward, coupling=coupling)
     alpha = ms.coupling_alpha(p["neur_coords"]).astype(np.float32)
     o = ko.Oracle(cfg, alpha)
     bins = kura.spectral.beta_bins(cfg.window, p["verbose_dt"])

@@ -67,16 +67,20 @@ def test_env2_n1024_vector_env(torch_gpu):
     env.close()
 
 
-@pytest.mark.parametrize("name,reward,steps", [("env0", "bbpow_action", 50), ("env1", "temp_const_action", 50),
-                                               ("env1", "bbpow_action", 50)])
-def test_full_grid_b4096_sampled(torch_gpu, name, reward, steps):
-    """configs[1]/[2] at full size: B=4096 (256 workgroups), reset + 50 steps;
+@pytest.mark.parametrize("name,reward,steps,coupling", [("env0", "bbpow_action", 24, "auto"),
+                                                        ("env1", "temp_const_action", 24, "auto"),
+                                                        ("env1", "bbpow_action", 16, "auto"),
+                                                        ("env0", "bbpow_action", 50, "f32")])
+def test_full_grid_b4096_sampled(torch_gpu, name, reward, steps, coupling):
+    """configs[1]/[2] at full size: B=4096 (256 workgroups), reset + steps;
     envs sampled from first, middle and last workgroups and across the
-    16-env interleave checked bit for bit against the oracle run on just them."""
+    16-env interleave checked bit for bit against the oracle run on just them
+    (the product arithmetic, and F32; the bf16x3 oracle costs ~0.5 s per
+    N=1024 step of these 14 envs, hence fewer steps)."""
     torch = torch_gpu
     sim_mod = importlib.import_module("dbs-gym_amd.sim")
     B, N = 4096, 1024
-    cfg, alpha, omega, gs, gr, th0, ct, st, _ = make_case(name, N, B, reward=reward)
+    cfg, alpha, omega, gs, gr, th0, ct, st, _ = make_case(name, N, B, reward=reward, coupling=coupling)
     sim = sim_mod.KuraSim(cfg, 0)
     sim.set_coupling(alpha)
     sim.set_env_params(omega, gs, gr)
@@ -194,7 +198,8 @@ def test_env2_phase_gate_1000_steps_vector_env(torch_gpu):
     300-step episodes (3 autoresets per env, each with the reference's drift
     draws), rewards every step and phases at the end bit-exact against the
     oracle (hence within 1e-5 relative), the reset draws replayed by fresh
-    EnvHosts."""
+    EnvHosts.  F32 coupling against the live oracle; the product arithmetic's
+    gate replays a committed oracle record (tests/test_gpu_gates.py)."""
     vec = importlib.import_module("dbs-gym_amd.vec_env")
     import copy
     B, N, L = 8, 1024, 300
@@ -206,7 +211,7 @@ def test_env2_phase_gate_1000_steps_vector_env(torch_gpu):
         p["K"] = float(Ks[b])
         p["rand_seed"] = 500 + b
         plist.append(p)
-    env = vec.KuraVectorEnv(plist, reward_func="bbpow_action")
+    env = vec.KuraVectorEnv(plist, reward_func="bbpow_action", coupling="f32")
     env.episode_steps = L
     c = copy.copy(env.cfg)
     o = ko.Oracle(c, env._alpha.astype(np.float32))

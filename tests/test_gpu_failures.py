@@ -272,3 +272,89 @@ def test_reset_failure_runs_count_consecutive_failures_only(torch_gpu, monkeypat
         assert calls["n"] >= 5
         assert env._reset_fail_runs[0] == 0
         env.close()
+
+
+def _short_env(venv, kura, n, steps, **kw):
+    p = kura.reference_params("env0", "eval", 0)
+    p["reward_func"] = "bbpow_action"
+    p["total_episode_len"] = steps * (p["electrode_width"] + p["electrode_pause"])
+    return venv.KuraVectorEnv(p, num_envs=n, on_failure="reset", failure_check="deferred", **kw)
+
+
+def _poison(env, b):
+    st = env.sim.get_state()
+    st["y"][b, 0] = np.nan
+    env.sim.set_state(st)
+
+
+def test_deferred_failure_on_terminal_step_same_step_resets_once(torch_gpu):
+    """an env whose last step of the episode fails is autoreset in
+    that call (same_step); the deferred check one call later reports the
+    failure but must not reset it a second time (an extra draw from its RNG
+    stream, and a bogus zero-length episode for an SB3 wrapper)."""
+    kura = importlib.import_module("dbs-gym_amd")
+    venv = importlib.import_module("dbs-gym_amd.vec_env")
+    env = _short_env(venv, kura, 3, 2)
+    env.reset()
+    a = np.zeros((3, 1), np.float32)
+    env.step(a)
+    _poison(env, 1)
+    obs, rew, term, trunc, info = env.step(a)                 # fails on the device; episode ends: autoreset
+    assert list(info["terminal_env_ids"]) == [0, 1, 2]
+    rc = [h.reset_count for h in env.hosts]
+    obs, rew, term, trunc, info = env.step(a)
+    assert list(info["failed_env_ids"]) == [1] and info["failure_flags"][0] == abi.KURA_F_NONFINITE
+    assert "reset_before_step_ids" not in info and not bool(trunc[1])
+    assert [h.reset_count for h in env.hosts] == rc           # no second reset
+    assert env.steps[1] == 1 and np.isfinite(rew.cpu().numpy()).all()
+    env.close()
+
+
+def test_deferred_failure_next_step_mode_ends_the_episode_then_resets(torch_gpu):
+    """ADVICE r04, gymnasium NEXT_STEP with deferred checks: the failure of
+    call k is reported in call k+1 as the episode's end (truncated, the last
+    observation, reward 0), and call k+2 resets the env (reset_env_ids) --
+    not a reset before the launch of call k+1."""
+    kura = importlib.import_module("dbs-gym_amd")
+    venv = importlib.import_module("dbs-gym_amd.vec_env")
+    env = _short_env(venv, kura, 3, 50, autoreset_mode="next_step")
+    env.reset()
+    a = np.zeros((3, 1), np.float32)
+    env.step(a)
+    _poison(env, 1)
+    obs_k, rew, term, trunc, info = env.step(a)               # fails on the device (not known yet)
+    assert "failed_env_ids" not in info and not bool(trunc[1])
+    rc = [h.reset_count for h in env.hosts]
+    obs, rew, term, trunc, info = env.step(a)                 # call k+1: the failed episode ends here
+    assert list(info["failed_env_ids"]) == [1]
+    assert bool(trunc[1]) and not bool(term[1]) and float(rew[1]) == 0.0
+    assert not bool(trunc[0]) and not bool(trunc[2])
+    np.testing.assert_array_equal(obs[1].cpu().numpy(), obs_k[1].cpu().numpy())   # its last observation
+    assert [h.reset_count for h in env.hosts] == rc           # not reset yet
+    obs, rew, term, trunc, info = env.step(a)                 # call k+2: reset
+    assert list(info["reset_env_ids"]) == [1] and float(rew[1]) == 0.0 and not bool(trunc[1])
+    assert "failed_env_ids" not in info                        # the discarded step's flags do not count
+    assert [h.reset_count for h in env.hosts] == [rc[0], rc[1] + 1, rc[2]]
+    obs, rew, term, trunc, info = env.step(a)
+    assert "failed_env_ids" not in info and np.isfinite(rew.cpu().numpy()).all() and env.steps[1] == 1
+    env.close()
+
+
+def test_deferred_failure_on_terminal_step_next_step_mode_resets_once(torch_gpu):
+    """next_step mode, the failing step is the episode's last: the
+    env is queued for its next_step reset; the deferred report must not reset
+    it before that reset as well."""
+    kura = importlib.import_module("dbs-gym_amd")
+    venv = importlib.import_module("dbs-gym_amd.vec_env")
+    env = _short_env(venv, kura, 3, 2, autoreset_mode="next_step")
+    env.reset()
+    a = np.zeros((3, 1), np.float32)
+    env.step(a)
+    _poison(env, 1)
+    obs, rew, term, trunc, info = env.step(a)                 # fails; the episode ends (counters)
+    assert bool(term[1])
+    rc = [h.reset_count for h in env.hosts]
+    obs, rew, term, trunc, info = env.step(a)                 # next_step resets + the deferred report
+    assert list(info["failed_env_ids"]) == [1] and list(info["reset_env_ids"]) == [0, 1, 2]
+    assert [h.reset_count for h in env.hosts] == [c + 1 for c in rc]
+    env.close()

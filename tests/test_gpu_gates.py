@@ -1,0 +1,127 @@
+"""The north_star gate in the product arithmetic: N=1024, 1000 steps, phases
+within 1e-5 relative of the oracle (BASELINE.json) -- here bit-exact, on the
+default coupling (KURA_COUPLING_AUTO = BF16X3 at N=1024), for env0/R1,
+env1/R2 and env2 through KuraVectorEnv with 3 autoresets per env.
+
+The oracle side is the committed record of tests/golden/make_gate_fixtures.py
+(the split-bf16 oracle costs ~0.5 s per N=1024 step of 8 envs; it runs once,
+in the build container); tests/test_gate_fixtures.py re-checks a prefix of
+each record against a live oracle on the CPU.  Compared: every step's
+rewards, a running SHA-1 over every output of every step (obs, reward, done,
+nsamp, lfp_true, lfp_rec), and the full state at steps 250/500/750/1000 and
+after each autoreset.  (The fp32-coupling gates run live against the fp32
+oracle in tests/test_gpu_parity.py.)"""
+from __future__ import annotations
+
+import copy
+import importlib
+import os
+
+import numpy as np
+import pytest
+
+import gate_scenarios as gs
+from helpers import actions, kura
+
+pytestmark = pytest.mark.gpu
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+PHASE_RTOL = 1e-5  # BASELINE.json north_star
+
+
+@pytest.fixture(scope="module")
+def torch_gpu():
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch
+
+
+def _record(name):
+    R = np.load(os.path.join(GOLDEN, f"gate_{name}.npz"))
+    assert str(R["coupling"]) == "bf16x3"
+    return R
+
+
+def _check_state(st, R, tag):
+    for k in gs.STATE_KEYS:
+        g, want = np.asarray(st[k]), R[f"{tag}_{k}"]
+        if not np.array_equal(g, want):
+            bad = np.argwhere(g != want)
+            raise AssertionError(f"{tag}: state[{k}] differs at {len(bad)} places, first {bad[:3].tolist()}")
+    assert gs.sha1(st["ring"]) == R[f"{tag}_ring_sha1"].tobytes().hex(), f"{tag}: ring"
+
+
+def _phase_gate(y, want):
+    rel = np.abs(y.astype(np.float64) - want) / np.maximum(np.abs(want.astype(np.float64)), 1e-30)
+    assert rel.max() <= PHASE_RTOL
+    np.testing.assert_array_equal(y, want)
+
+
+@pytest.mark.parametrize("scenario", ["env0_r1", "env1_r2"])
+def test_gate_1000_steps_product_arithmetic(torch_gpu, scenario):
+    torch = torch_gpu
+    R = _record(scenario)
+    name, reward, act = gs.SCENARIOS[scenario]
+    sim_mod = importlib.import_module("dbs-gym_amd.sim")
+    cfg, alpha, omega, g_s, g_r, th0, ct, st, _ = gs.env01_case(name, reward)
+    assert kura.coupling_of(cfg) == "bf16x3"       # the product default at N=1024
+    sim = sim_mod.KuraSim(cfg, 0)
+    sim.set_coupling(alpha)
+    sim.set_env_params(omega, g_s, g_r)
+    sim.set_spectral(ct, st)
+    obs0 = sim.reset(torch.from_numpy(th0)).cpu().numpy()
+    assert gs.sha1(obs0) == R["reset_obs_sha1"].tobytes().hex()
+    _check_state(sim.get_state(), R, "reset")
+    dig = gs.StepDigest()
+    for k in range(gs.STEPS):
+        sim.step(torch.from_numpy(actions(act, gs.B, cfg.n_elec, k)))
+        rew = sim.reward.cpu().numpy()
+        np.testing.assert_array_equal(rew, R["rewards"][k], err_msg=f"reward step {k}")
+        dig.add(sim.obs.cpu().numpy(), rew, sim.done.cpu().numpy(), sim.nsamp.cpu().numpy(),
+                sim.lfp_true.cpu().numpy(), sim.lfp_rec.cpu().numpy())
+        if k + 1 in gs.CHECK:
+            _check_state(sim.get_state(), R, f"s{k + 1}")
+            assert dig.hexdigest() == R[f"s{k + 1}_digest"].tobytes().hex(), f"outputs through step {k + 1}"
+    g = sim.get_state()
+    np.testing.assert_array_equal(g["ring"], R["final_ring"])
+    _phase_gate(g["y"], R["s1000_y"])
+    sim.close()
+
+
+def test_gate_1000_steps_env2_vector_env_product_arithmetic(torch_gpu):
+    """env2 (drift events, per-env K) through KuraVectorEnv, 300-step
+    episodes: 3 autoresets per env, each with the reference's drift draws."""
+    R = _record("env2_r1_vec")
+    vec = importlib.import_module("dbs-gym_amd.vec_env")
+    plist, _ = gs.env2_setup()
+    env = vec.KuraVectorEnv(copy.deepcopy(plist), reward_func="bbpow_action")
+    assert kura.coupling_of(env.cfg) == "bf16x3"
+    env.episode_steps = gs.ENV2_EPISODE
+    obs, _ = env.reset()
+    assert gs.sha1(obs[:, 0].cpu().numpy()) == R["reset_obs_sha1"].tobytes().hex()
+    _check_state(env.sim.get_state(), R, "reset")
+    dig = gs.StepDigest()
+    nres = 0
+    for k in range(gs.STEPS):
+        obs, rew, term, trunc, info = env.step(gs.env2_actions(k, env.cfg.n_elec))
+        r = rew.cpu().numpy()
+        np.testing.assert_array_equal(r, R["rewards"][k], err_msg=f"reward step {k}")
+        s = env.sim
+        step_obs = obs[:, 0]
+        if (k + 1) % gs.ENV2_EPISODE == 0:
+            nres += 1
+            assert len(info["terminal_env_ids"]) == gs.B
+            step_obs = info["terminal_observation"][:, 0]
+            assert gs.sha1(obs[:, 0].cpu().numpy()) == R[f"r{nres}_obs_sha1"].tobytes().hex(), f"reset {nres}"
+            _check_state(s.get_state(), R, f"r{nres}")
+        # (s.done: the kernel's done of the step; the reset kernel leaves it and the LFP outputs alone)
+        dig.add(step_obs.cpu().numpy(), r, s.done.cpu().numpy(), s.nsamp.cpu().numpy(),
+                s.lfp_true.cpu().numpy(), s.lfp_rec.cpu().numpy())
+        if k + 1 in gs.CHECK:
+            _check_state(s.get_state(), R, f"s{k + 1}")
+            assert dig.hexdigest() == R[f"s{k + 1}_digest"].tobytes().hex(), f"outputs through step {k + 1}"
+    assert nres == 3
+    g = env.sim.get_state()
+    np.testing.assert_array_equal(g["ring"], R["final_ring"])
+    _phase_gate(g["y"], R["s1000_y"])
+    env.close()

@@ -4,6 +4,11 @@ BASELINE.json's gate is 1e-5 relative on phases after 1000 steps; the HIP
 kernels are built as a bit-exact twin of oracle/kura_oracle.c (DESIGN.md
 "Numerics"), so every comparison here is exact equality, which implies the
 1e-5 tolerance (asserted explicitly in test_phase_gate_1000_steps).
+Both coupling arithmetics (kura.h KURA_COUPLING_*) are twins: the product
+default (AUTO = BF16X3 for N <= 1024) and F32; the oracle follows the
+config.  The 1000-step gates here run the F32 coupling against the live
+oracle; the product arithmetic's gates replay committed oracle records
+(tests/test_gpu_gates.py).
 """
 from __future__ import annotations
 
@@ -33,6 +38,7 @@ def lib(torch_gpu):
     L = abi.load_library()
     L.kura_selftest_math.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_int]
     L.kura_selftest_gemm.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_int]
+    L.kura_selftest_coupling.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_int] * 2
     return L
 
 
@@ -69,9 +75,29 @@ def test_mfma_gemm_is_fmaf_chain(lib, N):
     np.testing.assert_array_equal(Y, ko.gemm_chain(X, A))
 
 
-def _run_pair(torch, name, N, B, reward, steps, act, check_every=1, gains=None, **overrides):
+@pytest.mark.parametrize("N", [256, 512, 1024])
+def test_bf16x3_gemm_is_the_oracle_chain(lib, N):
+    """The product coupling GEMM (KURA_COUPLING_BF16X3, six bf16 MFMA part
+    products per 16-deep k-block) == oracle_split_gemm_rows bit for bit on
+    signed random operands, and as accurate as the fp32 chain (within 2x of
+    its worst error against the exact sum)."""
+    rng = np.random.default_rng(N + 1)
+    X = rng.uniform(-1, 1, (32, N)).astype(np.float32)
+    A = rng.uniform(-1, 1, (N, N)).astype(np.float32)
+    Y = np.zeros((32, N), np.float32)
+    assert lib.kura_selftest_coupling(X.ctypes.data, A.ctypes.data, Y.ctypes.data, N, 2) == 0
+    assert np.array_equal(Y.view(np.uint32), ko.split_gemm_rows(X, A).view(np.uint32))
+    exact = X.astype(np.float64) @ A.astype(np.float64).T
+    assert np.abs(Y - exact).max() <= 2.0 * np.abs(ko.gemm_chain(X, A) - exact).max() + 1e-6
+    Yf = np.zeros((32, N), np.float32)   # KURA_COUPLING_F32 through the same entry point
+    assert lib.kura_selftest_coupling(X.ctypes.data, A.ctypes.data, Yf.ctypes.data, N, 1) == 0
+    np.testing.assert_array_equal(Yf, ko.gemm_chain(X, A))
+
+
+def _run_pair(torch, name, N, B, reward, steps, act, check_every=1, gains=None, coupling="auto", **overrides):
     sim_mod = importlib.import_module("dbs-gym_amd.sim")
-    cfg, alpha, omega, gs, gr, th0, ct, st, _ = make_case(name, N, B, reward=reward, **overrides)
+    cfg, alpha, omega, gs, gr, th0, ct, st, _ = make_case(name, N, B, reward=reward, coupling=coupling,
+                                                          **overrides)
     sim = sim_mod.KuraSim(cfg, 0)
     sim.set_coupling(alpha)
     sim.set_env_params(omega, gs, gr)
@@ -112,15 +138,17 @@ def _cmp_state(g, o, where):
                                  f"gpu={g[k][tuple(bad[0])]!r} oracle={o[k][tuple(bad[0])]!r}")
 
 
-@pytest.mark.parametrize("name,N,reward,act", [
-    ("env0", 512, "bbpow_action", "rand"),
-    ("env1", 512, "bbpow_threth_action", "hf"),
-    ("env1", 512, "temp_const_action", "rand"),
-    ("env0", 256, "bbpow_action", "off"),
-    ("env0", 1024, "bbpow_action", "rand"),
+@pytest.mark.parametrize("name,N,reward,act,coupling", [
+    ("env0", 512, "bbpow_action", "rand", "auto"),
+    ("env1", 512, "bbpow_threth_action", "hf", "auto"),
+    ("env1", 512, "temp_const_action", "rand", "auto"),
+    ("env0", 256, "bbpow_action", "off", "auto"),
+    ("env0", 1024, "bbpow_action", "rand", "auto"),
+    ("env0", 512, "bbpow_action", "rand", "f32"),
+    ("env1", 256, "temp_const_action", "hf", "f32"),
 ])
-def test_step_parity_short(torch_gpu, name, N, reward, act):
-    _run_pair(torch_gpu, name, N, 19, reward, 12, act)
+def test_step_parity_short(torch_gpu, name, N, reward, act, coupling):
+    _run_pair(torch_gpu, name, N, 19, reward, 12, act, coupling=coupling)
 
 
 def test_step_parity_random_gain(torch_gpu):
@@ -140,8 +168,10 @@ def test_step_parity_wavelet_directed(torch_gpu):
 
 
 def test_phase_gate_1000_steps(torch_gpu):
-    """BASELINE.json gate: phases within 1e-5 relative after 1000 steps at N=1024."""
-    g, o = _run_pair(torch_gpu, "env0", 1024, 8, "bbpow_action", 1000, "rand", check_every=250)
+    """BASELINE.json gate: phases within 1e-5 relative after 1000 steps at
+    N=1024, F32 coupling against the live oracle (the product arithmetic:
+    tests/test_gpu_gates.py)."""
+    g, o = _run_pair(torch_gpu, "env0", 1024, 8, "bbpow_action", 1000, "rand", check_every=250, coupling="f32")
     rel = np.abs(g["y"].astype(np.float64) - o["y"]) / np.maximum(np.abs(o["y"].astype(np.float64)), 1e-30)
     assert rel.max() <= PHASE_RTOL
     np.testing.assert_array_equal(g["y"], o["y"])
@@ -150,7 +180,8 @@ def test_phase_gate_1000_steps(torch_gpu):
 def test_phase_gate_1000_steps_env1_r2(torch_gpu):
     """The same gate on env1 (recorder-weighted f64 LFP, per-env contacts) with
     the R2 filter reward at N=1024 (TPW=4 gaussian save passes)."""
-    g, o = _run_pair(torch_gpu, "env1", 1024, 8, "temp_const_action", 1000, "rand", check_every=250)
+    g, o = _run_pair(torch_gpu, "env1", 1024, 8, "temp_const_action", 1000, "rand", check_every=250,
+                     coupling="f32")
     rel = np.abs(g["y"].astype(np.float64) - o["y"]) / np.maximum(np.abs(o["y"].astype(np.float64)), 1e-30)
     assert rel.max() <= PHASE_RTOL
     np.testing.assert_array_equal(g["y"], o["y"])

@@ -35,11 +35,15 @@ Z_MAX = 1.5
 SD_BAND = 2.5
 
 
-def _run(name, episodes, overrides):
+COUPLINGS = ("f32", "bf16x3")   # KuraConfig.coupling: both arithmetics meet the paper
+
+
+def _run(name, episodes, overrides, coupling="f32"):
     for r in ORACLE:
-        if r["config"] == name and r["episodes"] == episodes and r["overrides"] == overrides:
+        if (r["config"] == name and r["episodes"] == episodes and r["overrides"] == overrides
+                and r.get("coupling", "f32") == coupling):
             return r
-    raise KeyError((name, episodes, overrides))
+    raise KeyError((name, episodes, overrides, coupling))
 
 
 def _z(name, arm, values):
@@ -59,10 +63,11 @@ def test_paper_table_transcription():
     assert all(PAPER[e]["hf"]["energy"] == 5555.0 for e in PAPER)   # 5 episodes x 1111 steps x |a| = 1
 
 
+@pytest.mark.parametrize("coupling", COUPLINGS)
 @pytest.mark.parametrize("name,overrides", [("env0", {}), ("env1", {}), ("env2", {}),
                                             ("env2", {"encapsulation_mode": "relative"})])
-def test_oracle_protocol_meets_paper(name, overrides):
-    r = _run(name, 5, overrides)
+def test_oracle_protocol_meets_paper(name, overrides, coupling):
+    r = _run(name, 5, overrides, coupling)
     z_off, z_hf = _z(name, "off", r["bbpow_off"]), _z(name, "hf", r["bbpow_hf"])
     assert abs(z_off) <= Z_MAX, (name, z_off)
     assert 1 / SD_BAND <= _sd_ratio(name, "off", r["bbpow_off"]) <= SD_BAND
@@ -86,16 +91,19 @@ def test_oracle_protocol_env0_one_episode():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name,overrides", [("env0", {}), ("env1", {}), ("env2", {}),
-                                            ("env2", {"encapsulation_mode": "relative"})])
-def test_gpu_protocol_matches_oracle_and_paper(name, overrides):
+@pytest.mark.parametrize("name,overrides,coupling", [("env0", {}, "bf16x3"), ("env1", {}, "bf16x3"),
+                                                     ("env2", {}, "bf16x3"),
+                                                     ("env2", {"encapsulation_mode": "relative"}, "bf16x3"),
+                                                     ("env0", {}, "f32")])
+def test_gpu_protocol_matches_oracle_and_paper(name, overrides, coupling):
     """The full protocol on the HIP path (5 envs x 2 arms in one batch, 5555
     steps with autoreset, episode metric on the GPU): per-env beta power equal
     to the oracle's (bit-exact trajectories; the metric itself is a float64
-    DFT vs pocketfft, 1e-9) and the paper rule."""
+    DFT vs pocketfft, 1e-9) and the paper rule -- in the product arithmetic
+    (bf16x3, the default at N=512) for every config, and in f32 for env0."""
     ev = importlib.import_module("dbs-gym_amd.evaluation")
-    res = ev.run_protocol(name, n_episodes=5, **overrides)
-    r = _run(name, 5, overrides)
+    res = ev.run_protocol(name, n_episodes=5, coupling=coupling, **overrides)
+    r = _run(name, 5, overrides, coupling)
     assert [len(s) for s in res["lfp"]] == r["signal_len"]
     np.testing.assert_allclose(res["bbpow"][0], r["bbpow_off"], rtol=1e-9)
     np.testing.assert_allclose(res["bbpow"][1], r["bbpow_hf"], rtol=1e-9)
