@@ -59,7 +59,7 @@ def test_stress_n8192_full_size_sampled(torch_gpu, envs, idx):
     args = types.SimpleNamespace(config="env0", osc=8192, envs=envs, seed=2024, random_k=False,
                                  reward="bbpow_action", part_osc=-1, coupling="auto")
     cfg, alpha, omega, g_s, g_r, th0, ct, st, gain = bench.build_shard(args, 0)
-    assert cfg.part_osc == (0 if envs == 1024 else 256)
+    assert cfg.part_osc == (1024 if envs == 1024 else 256)   # sim.auto_part_osc
     sim = sim_mod.KuraSim(cfg, 0)
     sim.set_coupling(alpha)
     sim.set_env_params(omega, g_s, g_r)
