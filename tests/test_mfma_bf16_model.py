@@ -127,7 +127,7 @@ def test_vectorised_split_gemm_equals_the_chain():
 
 
 def test_split_gemm_signed_alpha_and_binade_crossings():
-    """The split build's GEMM (kura_selftest_gemm of libkura_split.so, K1's k
+    """The bf16x3 GEMM (round 4's split build, now kura_selftest_coupling(.., 2) of libkura.so; K1's k
     order) on signed and on positive alpha, 3001 sampled outputs each, equals
     oracle_split_gemm_rows; and the two traced chains whose accumulator crosses
     a power of two -- the MFMAs that anchor the adder's 32-bit window on the

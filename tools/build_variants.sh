@@ -6,6 +6,3 @@ python -c "import __graft_entry__ as g; g.build()"
 cd dbs-gym_amd/csrc
 hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -ffp-contract=off -fno-fast-math -Wall -Wno-unused-function \
       -DKURA_STAMPS -o libkura_stamps.so kura_kernels.hip
-# the split-bf16 coupling experiment: not the product
-hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -ffp-contract=off -fno-fast-math -Wall -Wno-unused-function \
-      -DKURA_SPLIT_GEMM -o libkura_split.so kura_kernels.hip

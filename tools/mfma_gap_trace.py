@@ -16,7 +16,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "tools"))
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 from helpers import make_case  # noqa: E402
-import split_k1_check as sk  # noqa: E402
+import split_gemm_check as sk  # noqa: E402
 
 TRACE = os.path.join(ROOT, "tools", "mfma_chain_trace")
 out = {"xp": [], "ap": [], "acc": [], "want": [], "model": [], "src": []}
@@ -27,7 +27,7 @@ for f in sys.argv[1:]:
     _, alpha, *_ = make_case("env0", N, 16, coupling="bf16x3")
     perm = (np.arange(N).reshape(-1, 16)[:, np.r_[0:16:2, 1:16:2]]).ravel()
     for r, c in np.argwhere(Y.view(np.uint32) != W.view(np.uint32)):
-        xp, ap = sk.bf16_split3(X[r, perm]), sk.bf16_split3(alpha[c, perm])
+        xp, ap = sk.split3(X[r, perm]), sk.split3(alpha[c, perm])
         with tempfile.TemporaryDirectory() as t:
             fi, fo = os.path.join(t, "in.bin"), os.path.join(t, "out.bin")
             with open(fi, "wb") as fh:

@@ -15,8 +15,8 @@ sys.path.insert(0, ROOT)
 import __graft_entry__ as ge  # noqa: E402
 
 SI = os.environ.get("SI") == "1"  # stage-input sub-phases (KURA_STAMPS_SI build, no record prefetch)
-SPLIT = os.environ.get("SPLIT") == "1"  # the split-bf16 coupling experiment (KURA_SPLIT_GEMM)
-LIB = os.path.join(ge.CSRC, "libkura_stamps_si.so" if SI else "libkura_stamps_split.so" if SPLIT else "libkura_stamps.so")
+COUPLING = os.environ.get("COUPLING", "auto")  # auto | f32 | bf16x3 (KuraConfig.coupling, a run-time choice)
+LIB = os.path.join(ge.CSRC, "libkura_stamps_si.so" if SI else "libkura_stamps.so")
 PHASES = ["stage_input", "barrier1", "gemm", "epilogue", "barrier2", "post_err", "flag_sync", "post_decide",
           "post_saves", "post_fsal", "post_time", "save_setup", "save_loadwait", "save_compute", "save_publish",
           "save_totals", "si_load", "si_compute", "si_lds", "si_misc", "tail_window", "tail_reward", "tail_other",
@@ -26,7 +26,7 @@ PHASES = ["stage_input", "barrier1", "gemm", "epilogue", "barrier2", "post_err",
 def main():
     if not os.path.exists(LIB) or os.path.getmtime(LIB) < os.path.getmtime(os.path.join(ge.CSRC, "kura_kernels.hip")):
         subprocess.run([ge.HIPCC, *ge.HIP_FLAGS, "-DKURA_STAMPS", *(["-DKURA_STAMPS_SI"] if SI else []),
-                        *(["-DKURA_SPLIT_GEMM"] if SPLIT else []), "-o", LIB,
+                        "-o", LIB,
                         os.path.join(ge.CSRC, "kura_kernels.hip")], check=True)
     import numpy as np
     import torch
@@ -40,6 +40,7 @@ def main():
         reward = os.environ.get("REWARD", "bbpow_action")
         seed = 7
         random_k = False
+        coupling = COUPLING
     cfg, alpha, omega, gs, gr, th0, ct, st, gain = bench.build_shard(A, 0)
     sim = sim_mod.KuraSim(cfg, 0, lib_path=LIB)
     sim.set_coupling(alpha)

@@ -3,7 +3,6 @@ model disagree: many random (X, A) at N = 1024 with sin/cos-like rows and
 cos-of-distance-like or signed A; writes every mismatching chain (K1 k
 order) as a trace input for tools/mfma_chain_trace.
     python tools/split_gemm_hunt.py OUTDIR [n_gemms]"""
-import ctypes
 import importlib
 import os
 import sys
@@ -14,11 +13,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tools"))
 from oracle import kura_oracle as ko  # noqa: E402
-import split_k1_check as sk  # noqa: E402
+import split_gemm_check as sk  # noqa: E402
 
 abi = importlib.import_module("dbs-gym_amd.abi")
-L = abi.load_library(os.path.join(ROOT, "dbs-gym_amd", "csrc", "libkura_split.so"))
-L.kura_selftest_gemm.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_int]
+L = abi.load_library()   # the bf16x3 GEMM through kura_selftest_coupling (KURA_COUPLING_BF16X3 = 2)
 out, n = sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else 40
 os.makedirs(out, exist_ok=True)
 N = 1024
@@ -36,13 +34,13 @@ for seed in range(n):
     else:
         A = (rng.uniform(0.3, 1, (N, N)) * np.where(rng.random((N, N)) < 0.1, -1, 1)).astype(np.float32)
     Y = np.zeros((32, N), np.float32)
-    assert L.kura_selftest_gemm(X.ctypes.data, A.ctypes.data, Y.ctypes.data, N) == 0
+    assert L.kura_selftest_coupling(X.ctypes.data, A.ctypes.data, Y.ctypes.data, N, 2) == 0
     W = ko.split_gemm_rows(X, A)
     bad = np.argwhere(Y.view(np.uint32) != W.view(np.uint32))
     tot += Y.size
     bad_n += len(bad)
     for r, c in bad[:4]:
-        xp, ap = sk.bf16_split3(X[r, perm]), sk.bf16_split3(A[c, perm])
+        xp, ap = sk.split3(X[r, perm]), sk.split3(A[c, perm])
         with open(os.path.join(out, f"s{seed}_r{r}_c{c}.bin"), "wb") as fh:
             np.array([N], np.int32).tofile(fh)
             xp.astype(np.uint16).tofile(fh)
