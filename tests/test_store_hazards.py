@@ -66,7 +66,7 @@ def test_shipped_libraries_are_hazard_free(name):
     lib = os.path.join(CSRC, name)
     if not os.path.exists(lib):
         pytest.skip(f"{name} not built")
-    n, hz = chk.check_library(lib)
+    n, hz, _census = chk.check_library(lib)
     assert n > 100            # the records' wide stores are there
     assert not hz, hz[:5]
 
@@ -86,6 +86,22 @@ def test_old_sgpr_soffset_store_form_is_flagged(tmp_path):
     lib = str(tmp_path / "libkura_sgpr.so")
     subprocess.run([ge.HIPCC, *ge.HIP_FLAGS, "-o", lib, str(d / "dbs-gym_amd" / "csrc" / "kura_kernels.hip")],
                    check=True, capture_output=True)
-    _n, hz = chk.check_library(lib)
+    _n, hz, _census = chk.check_library(lib)
     assert hz, "the checker did not flag the SGPR-soffset store form"
     assert any(h[2] == "buffer_store_dwordx4" for h in hz)
+
+
+def test_spilled_mask_census_reads_compiler_listings():
+    """The round-4 lost-store shape: a store under an
+    exec mask restored from a spill lane is counted; a mask that is
+    overwritten after the restore, or one computed in place, is not."""
+    asm = "\n".join(["f:", "\tv_readlane_b32 s0, v252, 59", "\tv_readlane_b32 s1, v252, 60",
+                     "\ts_and_saveexec_b64 s[22:23], s[0:1]", "\tflat_store_dword v[12:13], v163",
+                     "\ts_or_b64 exec, exec, s[22:23]",
+                     "\tv_readlane_b32 s0, v252, 61", "\tv_readlane_b32 s1, v252, 62", "\ts_mov_b32 s1, 0",
+                     "\ts_and_saveexec_b64 s[22:23], s[0:1]", "\tflat_store_dword v[12:13], v160",
+                     "\ts_or_b64 exec, exec, s[22:23]",
+                     "\ts_and_saveexec_b64 s[22:23], s[14:15]", "\tflat_store_dword v[12:13], v162",
+                     "\ts_or_b64 exec, exec, s[22:23]"])
+    r = chk.find_spilled_store_masks(chk.parse_asm(asm))
+    assert [(n, v, k) for n, _i, v, k in r] == [("f", "v252", 1)]

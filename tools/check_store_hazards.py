@@ -164,13 +164,77 @@ def find_hazards(funcs):
     return out
 
 
+_SREG = re.compile(r"^s(\d+)$|^s\[(\d+):(\d+)\]$")
+_MASKED_STORE = re.compile(r"^(buffer|global|flat)_store_")
+
+
+def _sregs(tok: str) -> set[int]:
+    m = _SREG.match(tok.strip())
+    if not m:
+        return set()
+    if m.group(1) is not None:
+        return {int(m.group(1))}
+    return set(range(int(m.group(2)), int(m.group(3)) + 1))
+
+
+def parse_asm(text: str):
+    """-> the parse() form from compiler assembly (hipcc -S) instead of a
+    disassembly: the round-4 failing build survives only as such a listing."""
+    funcs, cur = [], None
+    for line in text.splitlines():
+        if re.match(r"^[A-Za-z_][\w.$]*:", line) and not line.startswith(".L"):
+            cur = (line.split(":")[0], [])
+            funcs.append(cur)
+            continue
+        if cur is None or not line.startswith("\t") or line.strip().startswith((".", ";")):
+            continue
+        body = line.split(";")[0].strip()
+        if not body:
+            continue
+        mnem, _, rest = body.partition(" ")
+        cur[1].append((len(cur[1]), mnem, _operands(rest), None))
+    return funcs
+
+
+def find_spilled_store_masks(funcs):
+    """Census (not a gate) of the round-4 lost-store shape: a VMEM
+    store (buffer/global/flat) under an exec mask that s_and_saveexec_b64 took
+    from an SGPR pair restored by v_readlane_b32 from a spill lane.  Returns
+    (function, index of the s_and_saveexec, lane register, stores guarded).
+    Straight-line scan: a restored pair stays 'from a lane' until an
+    instruction whose first operand writes one of its registers."""
+    out = []
+    for name, insns in funcs:
+        lane = {}                       # sgpr -> spill VGPR it was read from
+        for i, (_a, mnem, ops, _t) in enumerate(insns):
+            if not ops:
+                continue
+            if mnem == "v_readlane_b32":
+                for r in _sregs(ops[0]):
+                    lane[r] = ops[1]
+                continue
+            if mnem == "s_and_saveexec_b64" and len(ops) > 1:
+                src = _sregs(ops[1])
+                if src and all(r in lane for r in src):
+                    dst, n = ops[0], 0
+                    for _b, m2, o2, _t2 in insns[i + 1:i + 40]:
+                        if m2 == "s_or_b64" and o2[:1] == ["exec"] and o2[-1] == dst:
+                            break
+                        n += bool(_MASKED_STORE.match(m2))
+                    if n:
+                        out.append((name, i, lane[min(src)], n))
+            for r in _sregs(ops[0]):
+                lane.pop(r, None)
+    return out
+
+
 def check_library(lib: str):
     """(number of wide VMEM stores, hazards) of a built HIP library."""
     with tempfile.TemporaryDirectory() as d:
         text = disassemble(code_object(lib, d))
     funcs = parse(text)
     nstores = sum(1 for _n, ins in funcs for (_a, m, _o, _t) in ins if _WIDE_STORE.match(m))
-    return nstores, find_hazards(funcs)
+    return nstores, find_hazards(funcs), find_spilled_store_masks(funcs)
 
 
 def main(argv):
@@ -182,11 +246,14 @@ def main(argv):
             print(f"{lib}: missing")
             bad += 1
             continue
-        n, hz = check_library(lib)
-        print(f"{os.path.basename(lib)}: {n} wide VMEM stores, {len(hz)} store-data hazards")
+        n, hz, sm = check_library(lib)
+        print(f"{os.path.basename(lib)}: {n} wide VMEM stores, {len(hz)} store-data hazards, "
+              f"{len(sm)} stores under a spilled exec mask")
         for name, a, m, o, b, bm, ws in hz[:20]:
             print(f"  {name}: {m} {o} @0x{a:x} <- {bm} @0x{b:x} after {ws} wait state(s)")
-        bad += bool(hz)
+        for name, i, v, k in sm[:20]:
+            print(f"  {name}: {k} store(s) under a mask read back from {v} (instruction {i})")
+        bad += bool(hz)   # the spilled-mask census is reported, not gated
     return 1 if bad else 0
 
 
