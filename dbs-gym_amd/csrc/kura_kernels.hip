@@ -174,6 +174,16 @@ __shared__ double s_smp_r[E_WG][KURA_S_MAX + 2];
 #ifndef KURA_XL_DEPTH4
 #define KURA_XL_DEPTH4 4
 #endif
+// ... and of its bf16x3 form, in 16-deep k-blocks (12 VGPRs per tile each)
+#ifndef KURA_XL_SP_DEPTH1
+#define KURA_XL_SP_DEPTH1 8
+#endif
+#ifndef KURA_XL_SP_DEPTH2
+#define KURA_XL_SP_DEPTH2 4
+#endif
+#ifndef KURA_XL_SP_DEPTH4
+#define KURA_XL_SP_DEPTH4 2
+#endif
 __host__ __device__ constexpr int xs_floats(int N) { return (N / 8) * XS_BLOCK; }
 // floats of one part's LDS / global sin/cos image (TPW column tiles per wave)
 __host__ __device__ constexpr int xl_img(int tpw) { return xs_floats(tpw * 256); }
@@ -510,6 +520,121 @@ __device__ __forceinline__ void coupling_gemm_xl(const float* __restrict__ xg, c
     }
 }
 
+
+// The split-group GEMM in KURA_COUPLING_BF16X3: coupling_gemm_bf16x3's chain
+// (six part products per 16-deep k-block, k ascending over all NG
+// oscillators, so P/Q are the oracle's oracle_split_gemm_rows at any N) with
+// the sin/cos operand streamed chunk by chunk as in coupling_gemm_xl and the
+// pre-split alpha (split_alpha, full-N column tiles) of this workgroup's
+// TPW*256 columns through a ring of XD k-blocks per tile.
+template <int TPW>
+__device__ __forceinline__ void coupling_gemm_xl_bf16x3(const float* __restrict__ xg, const float* __restrict__ alpha_sw,
+                                                        float* Xs, int NG, int col0, floatx16 (&acc)[TPW],
+                                                        unsigned long long* dbg STAMP_PARAMS) {
+    (void)dbg;
+    NG = __builtin_amdgcn_readfirstlane(NG);
+    col0 = __builtin_amdgcn_readfirstlane(col0);
+    xg = uniform_ptr(xg);
+    const int NB = NG / 16;
+    const int TSTRIDE = NB * 3 * 64 * 16;   // bytes per column tile
+    const int nchunk = NG / XL_KC;
+    int lane;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+#pragma unroll
+    for (int t = 0; t < TPW; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[t][r] = 0.0f;
+    const float* au = uniform_ptr(alpha_sw);
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)((const char*)au + ((size_t)(col0 / 32) + wave * TPW) * TSTRIDE), 0, TPW * TSTRIDE, 0x00020000);
+    auto ld = [&](int t, int b, int p) -> bf16x8 {
+        KDBG_CHECK(dbg, b >= 0 && b < NB && ((b * 3 + p) * 64 + lane) * 16 + t * TSTRIDE + 16 <= TPW * TSTRIDE);
+        return __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rs, ((b * 3 + p) * 64 + lane) * 16,
+                                                                                 t * TSTRIDE, 0));
+    };
+    constexpr int C4 = XL_CIMG / 4;
+    constexpr int CPT = (C4 + NTHREADS - 1) / NTHREADS;
+    gfloatx4* xg4 = (gfloatx4*)xg;
+    floatx4* xs4w = (floatx4*)Xs;
+    for (int k = threadIdx.x; k < C4; k += NTHREADS) xs4w[k] = xg4[k];
+    lds_barrier();
+    STAMP(18);
+    constexpr int XD = TPW >= 4 ? KURA_XL_SP_DEPTH4 : (TPW == 2 ? KURA_XL_SP_DEPTH2 : KURA_XL_SP_DEPTH1);
+    constexpr int KPC = XL_KC / 16;                // 16-deep k-blocks per chunk
+    constexpr int PRE = (CPT + XD - 1) / XD * XD;
+    static_assert(KPC % XD == 0 && PRE <= KPC, "alpha ring must tile the chunk");
+    bf16x8 q1[XD][TPW], q2[XD][TPW], q3[XD][TPW];
+#pragma unroll
+    for (int d = 0; d < XD; ++d)
+#pragma unroll
+        for (int t = 0; t < TPW; ++t) {
+            q1[d][t] = ld(t, d, 0);
+            q2[d][t] = ld(t, d, 1);
+            q3[d][t] = ld(t, d, 2);
+        }
+    floatx4 an0, an1;   // the next k-block's two float4 of the operand (LDS, one block ahead)
+    auto kblock = [&](const floatx4* xs4, int kg0, int kb, int d) __attribute__((always_inline)) {
+        const floatx4 lo = an0, hi = an1;
+        const int nb = kb + 1 < KPC ? kb + 1 : KPC - 1;
+        an0 = xs4[(2 * nb) * (XS_BLOCK / 4)];
+        an1 = xs4[(2 * nb + 1) * (XS_BLOCK / 4)];
+        bf16x8 x1, x2, x3;
+        split_bf16x3(lo, hi, x1, x2, x3);
+#pragma unroll
+        for (int t = 0; t < TPW; ++t) {
+            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x1, q1[d][t], acc[t], 0, 0, 0);
+            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x1, q2[d][t], acc[t], 0, 0, 0);
+            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x2, q1[d][t], acc[t], 0, 0, 0);
+            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x1, q3[d][t], acc[t], 0, 0, 0);
+            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x2, q2[d][t], acc[t], 0, 0, 0);
+            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x3, q1[d][t], acc[t], 0, 0, 0);
+        }
+        const int kn = kg0 + kb + XD < NB ? kg0 + kb + XD : NB - 1;
+#pragma unroll
+        for (int t = 0; t < TPW; ++t) {
+            q1[d][t] = ld(t, kn, 0);
+            q2[d][t] = ld(t, kn, 1);
+            q3[d][t] = ld(t, kn, 2);
+        }
+    };
+#pragma unroll 1
+    for (int c = 0; c < nchunk; ++c) {
+        const floatx4* xs4 = reinterpret_cast<const floatx4*>(Xs + (c & 1) * XL_CIMG + (lane >> 5) * XS_HALF +
+                                                              (lane & 31) * 4);
+        const int kg0 = c * KPC;
+        const bool more = c + 1 < nchunk;
+        an0 = xs4[0];
+        an1 = xs4[XS_BLOCK / 4];
+        floatx4 nx[CPT];
+#pragma unroll
+        for (int kb = 0; kb < PRE; ++kb) {
+            kblock(xs4, kg0, kb, kb % XD);
+            const int k = threadIdx.x + kb * NTHREADS;
+            if (kb < CPT && more && k < C4) nx[kb] = xg4[(size_t)(c + 1) * C4 + k];
+            __builtin_amdgcn_sched_barrier(0);
+        }
+#pragma unroll 1
+        for (int kb = PRE; kb < KPC; kb += XD) {
+#pragma unroll
+            for (int d = 0; d < XD; ++d) {
+                kblock(xs4, kg0, kb + d, d);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+        if (more) {
+            floatx4* dst = (floatx4*)(Xs + ((c + 1) & 1) * XL_CIMG);
+#pragma unroll
+            for (int u = 0; u < CPT; ++u) {
+                const int k = threadIdx.x + u * NTHREADS;
+                if (k < C4) dst[k] = nx[u];
+            }
+        }
+        STAMP(2);
+        lds_barrier();
+        STAMP(17);
+    }
+}
 
 // Per-env solver control.  One slot per local env lives in LDS; thread e
 // (e < 16) owns slot e's scalar decisions, every lane reads it.
@@ -1641,7 +1766,6 @@ __device__ KURA_SOLVE_ATTR void solve_wg(DevParamsK& __restrict__ pin, float* Xs
     // Made wave-uniform -- scalar loads, which share lgkmcnt with the LDS
     // traffic -- the step was 1.5 % slower in the same-box A/B,
     // profiles/r04_solver_ab.txt)
-    static_assert(!(XL && SP), "split env groups run the F32 coupling");
     DevParamsK& __restrict__ p = pin;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, tid = threadIdx.x;
     constexpr int N = TPW * 256;            // oscillators owned by this workgroup
@@ -1688,7 +1812,14 @@ __device__ KURA_SOLVE_ATTR void solve_wg(DevParamsK& __restrict__ pin, float* Xs
             const float* xgrp = uniform_ptr(group_publish_x<TPW>(p, pt, Xs));   // all parts' images of this stage
             xown = xgrp + (size_t)__builtin_amdgcn_readfirstlane(pt.part) * xl_img(TPW);
             STAMP(16);  // split groups: image publish + group barrier (slot 16 is free outside KURA_STAMPS_SI)
-            coupling_gemm_xl<TPW>(xgrp, p.alpha_sw, Xs, NG, col0, acc STAMP_ARGS);
+            if constexpr (SP)
+#ifdef KURA_DEBUG
+                coupling_gemm_xl_bf16x3<TPW>(xgrp, p.alpha_sw, Xs, NG, col0, acc, uniform_ptr(p.stats) STAMP_ARGS);
+#else
+                coupling_gemm_xl_bf16x3<TPW>(xgrp, p.alpha_sw, Xs, NG, col0, acc, nullptr STAMP_ARGS);
+#endif
+            else
+                coupling_gemm_xl<TPW>(xgrp, p.alpha_sw, Xs, NG, col0, acc STAMP_ARGS);
         } else {
 #ifdef KURA_DEBUG
             coupling_gemm<TPW, SP>(Xs, p.alpha_sw, acc, uniform_ptr(p.stats));

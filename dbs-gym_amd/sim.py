@@ -93,9 +93,6 @@ def make_config(params: dict, n_envs: int, reward_func: str | None = None, max_s
     if coupling not in abi.COUPLINGS:
         raise ValueError(f"coupling={coupling!r}: expected one of {sorted(abi.COUPLINGS)}")
     c.coupling = abi.COUPLINGS[coupling]
-    if abi.coupling_of(c) == "bf16x3" and c.n_osc > 1024:
-        raise NotImplementedError("coupling='bf16x3' with num_oscillators > 1024: split env groups run the "
-                                  "f32 coupling")
     if W < KURA_S_MAX:   # kura_create: a step's samples never wrap the ring twice
         raise ValueError(f"observation window of {W} samples: libkura needs at least {KURA_S_MAX} "
                          "(observe_wind_counts * (electrode_width + electrode_pause) / verbose_dt)")

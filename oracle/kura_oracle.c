@@ -261,14 +261,15 @@ void oracle_destroy(void* p) {
  * from the config through kura_coupling_of, as kura_create does): on = 1 is
  * KURA_COUPLING_BF16X3, P and Q from three-way bf16 splits on the bf16 MFMA's
  * exact accumulation (oracle_split_gemm_rows); on = 0 the fp32 fmaf chain.
- * N <= 1024 (split env groups run the fp32 coupling). */
+ * Any N (a multiple of 16): the split-group kernel's chain runs k ascending
+ * over all N oscillators, as the single-group one does. */
 int oracle_set_split(void* ctx, int on) {
     OCtx* o = (OCtx*)ctx;
     oracle_split_free(o->split);
     o->split = NULL;
     if (!on) return KURA_OK;
     const int N = o->N;
-    if (N > 1024 || N % 16) return KURA_E_UNSUPPORTED;
+    if (N % 16) return KURA_E_UNSUPPORTED;
     float* A = (float*)malloc(sizeof(float) * (size_t)N * N);
     if (!A) return KURA_E_NOMEM;
     for (int j = 0; j < N; ++j)

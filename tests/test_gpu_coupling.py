@@ -55,17 +55,16 @@ def test_each_coupling_is_a_twin_and_they_differ(torch_gpu):
     assert np.abs(y32.astype(np.float64) - ysp).max() < 1e-2   # 3 steps: still close
 
 
-def test_bf16x3_refused_for_split_groups(torch_gpu):
-    """n_osc > 1024 runs the F32 coupling: an explicit BF16X3 request is
-    refused by make_config and by kura_create itself (KURA_E_UNSUPPORTED)."""
+def test_split_groups_take_either_coupling(torch_gpu):
+    """n_osc > 1024: AUTO is F32; an explicit BF16X3 request builds the
+    split-group bf16x3 kernels (parity: tests/test_gpu_split.py); an unknown
+    value is refused."""
     sim_mod = importlib.import_module("dbs-gym_amd.sim")
-    with pytest.raises(NotImplementedError):
-        make_case("env0", 2048, 2, coupling="bf16x3")
     cfg, *_ = make_case("env0", 2048, 2)
     assert kura.coupling_of(cfg) == "f32"
     cfg.coupling = kura.abi.KURA_COUPLING_BF16X3
-    with pytest.raises(NotImplementedError, match="F32"):
-        sim_mod.KuraSim(cfg, 0)
+    assert kura.coupling_of(cfg) == "bf16x3"
+    sim_mod.KuraSim(cfg, 0).close()
     cfg.coupling = 7
     with pytest.raises(ValueError, match="coupling=7"):
         sim_mod.KuraSim(cfg, 0)
