@@ -94,7 +94,8 @@ enum { KURA_REC_NAIVE = 0, KURA_REC_GAUSSIAN = 1 };             /* env.py:333-33
  *           round-to-nearest-even, exact residuals), the six products
  *           x1a1, x1a2, x2a1, x1a3, x2a2, x3a1 per 16-deep k-block on
  *           v_mfma_f32_32x32x16_bf16 with fp32 accumulation (the oracle
- *           restates that MFMA's accumulation exactly); ~1.4x the F32 rate;
+ *           restates that MFMA's accumulation exactly); ~1.4x the F32 rate
+ *           at n_osc <= 1024; any n_osc (split env groups included);
  *   AUTO    BF16X3 for n_osc <= 1024, F32 above (split env groups). */
 enum { KURA_COUPLING_AUTO = 0, KURA_COUPLING_F32 = 1, KURA_COUPLING_BF16X3 = 2 };
 /* kura_coupling_of(cfg), below: the arithmetic a config resolves to (the
