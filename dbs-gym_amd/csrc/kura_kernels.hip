@@ -523,10 +523,16 @@ __device__ __forceinline__ void coupling_gemm_xl(const float* __restrict__ xg, c
 
 // The split-group GEMM in KURA_COUPLING_BF16X3: coupling_gemm_bf16x3's chain
 // (six part products per 16-deep k-block, k ascending over all NG
-// oscillators, so P/Q are the oracle's oracle_split_gemm_rows at any N) with
-// the sin/cos operand streamed chunk by chunk as in coupling_gemm_xl and the
-// pre-split alpha (split_alpha, full-N column tiles) of this workgroup's
-// TPW*256 columns through a ring of XD k-blocks per tile.
+// oscillators, so P/Q are the oracle's oracle_split_gemm_rows at any N),
+// with the pre-split alpha (split_alpha, full-N column tiles) of this
+// workgroup's TPW*256 columns through a ring of XD k-blocks per tile.  The
+// sin/cos operand is split ONCE per chunk, while it is staged: each thread
+// loads the two float4 of (k-block, lane) pairs from the group image and
+// writes their three bf16 parts to LDS, so the k-block loop reads x1/x2/x3
+// with three ds_read_b128 (splitting per k-block in every wave was 8x
+// redundant and made the TPW = 1 loop VALU-bound: ~57 VALU per 6 MFMAs).
+// Chunks are XL_KC_SP oscillators (two split buffers of 48 KB).
+#define XL_KC_SP 256
 template <int TPW>
 __device__ __forceinline__ void coupling_gemm_xl_bf16x3(const float* __restrict__ xg, const float* __restrict__ alpha_sw,
                                                         float* Xs, int NG, int col0, floatx16 (&acc)[TPW],
@@ -537,7 +543,13 @@ __device__ __forceinline__ void coupling_gemm_xl_bf16x3(const float* __restrict_
     xg = uniform_ptr(xg);
     const int NB = NG / 16;
     const int TSTRIDE = NB * 3 * 64 * 16;   // bytes per column tile
-    const int nchunk = NG / XL_KC;
+    constexpr int KC = XL_KC_SP;
+    constexpr int NBC = KC / 16;            // k-blocks per chunk
+    constexpr int CB = NBC * 3 * 64;        // bf16x8 per chunk buffer
+    constexpr int PAIRS = NBC * 64;         // (k-block, lane) pairs per chunk
+    constexpr int PPT = PAIRS / NTHREADS;
+    static_assert(PAIRS % NTHREADS == 0 && 2 * CB * 16 <= 2 * XL_CIMG * 4, "split chunks must fit the XL LDS");
+    const int nchunk = NG / KC;
     int lane;
     asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -553,17 +565,34 @@ __device__ __forceinline__ void coupling_gemm_xl_bf16x3(const float* __restrict_
         return __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rs, ((b * 3 + p) * 64 + lane) * 16,
                                                                                  t * TSTRIDE, 0));
     };
-    constexpr int C4 = XL_CIMG / 4;
-    constexpr int CPT = (C4 + NTHREADS - 1) / NTHREADS;
     gfloatx4* xg4 = (gfloatx4*)xg;
-    floatx4* xs4w = (floatx4*)Xs;
-    for (int k = threadIdx.x; k < C4; k += NTHREADS) xs4w[k] = xg4[k];
+    bf16x8* xsb = reinterpret_cast<bf16x8*>(Xs);
+    // the f32 float4 of pair pr (k-block pr/64 of chunk c, lane pr%64), half h
+    // (k8-block 2b + h): the XS layout of the group image
+    auto src = [&](int c, int pr, int h) -> size_t {
+        const int b = pr >> 6, l = pr & 63;
+        return ((size_t)c * (KC / 8) + 2 * b + h) * (XS_BLOCK / 4) + (l >> 5) * (XS_HALF / 4) + (l & 31);
+    };
+    auto put = [&](int buf, int pr, floatx4 lo, floatx4 hi) {
+        bf16x8 x1, x2, x3;
+        split_bf16x3(lo, hi, x1, x2, x3);
+        const int b = pr >> 6, l = pr & 63;
+        bf16x8* d = xsb + buf * CB + b * 3 * 64 + l;
+        d[0] = x1;
+        d[64] = x2;
+        d[128] = x3;
+    };
+#pragma unroll
+    for (int u = 0; u < PPT; ++u) {
+        const int pr = threadIdx.x + u * NTHREADS;
+        put(0, pr, xg4[src(0, pr, 0)], xg4[src(0, pr, 1)]);
+    }
     lds_barrier();
     STAMP(18);
     constexpr int XD = TPW >= 4 ? KURA_XL_SP_DEPTH4 : (TPW == 2 ? KURA_XL_SP_DEPTH2 : KURA_XL_SP_DEPTH1);
-    constexpr int KPC = XL_KC / 16;                // 16-deep k-blocks per chunk
-    constexpr int PRE = (CPT + XD - 1) / XD * XD;
-    static_assert(KPC % XD == 0 && PRE <= KPC, "alpha ring must tile the chunk");
+    constexpr int NX = 2 * PPT;                    // staging loads per thread and chunk
+    constexpr int PRE = (NX + XD - 1) / XD * XD;   // unrolled head: one staging load per k-block
+    static_assert(NBC % XD == 0 && PRE <= NBC, "alpha ring must tile the chunk");
     bf16x8 q1[XD][TPW], q2[XD][TPW], q3[XD][TPW];
 #pragma unroll
     for (int d = 0; d < XD; ++d)
@@ -573,14 +602,14 @@ __device__ __forceinline__ void coupling_gemm_xl_bf16x3(const float* __restrict_
             q2[d][t] = ld(t, d, 1);
             q3[d][t] = ld(t, d, 2);
         }
-    floatx4 an0, an1;   // the next k-block's two float4 of the operand (LDS, one block ahead)
-    auto kblock = [&](const floatx4* xs4, int kg0, int kb, int d) __attribute__((always_inline)) {
-        const floatx4 lo = an0, hi = an1;
-        const int nb = kb + 1 < KPC ? kb + 1 : KPC - 1;
-        an0 = xs4[(2 * nb) * (XS_BLOCK / 4)];
-        an1 = xs4[(2 * nb + 1) * (XS_BLOCK / 4)];
-        bf16x8 x1, x2, x3;
-        split_bf16x3(lo, hi, x1, x2, x3);
+    bf16x8 n1, n2, n3;   // the next k-block's operand parts (LDS, one block ahead)
+    auto kblock = [&](const bf16x8* xb, int kg0, int kb, int d) __attribute__((always_inline)) {
+        const bf16x8 x1 = n1, x2 = n2, x3 = n3;
+        const int nb = kb + 1 < NBC ? kb + 1 : NBC - 1;
+        n1 = xb[nb * 192];
+        n2 = xb[nb * 192 + 64];
+        n3 = xb[nb * 192 + 128];
+        const int kn = kg0 + kb + XD < NB ? kg0 + kb + XD : NB - 1;
 #pragma unroll
         for (int t = 0; t < TPW; ++t) {
             acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x1, q1[d][t], acc[t], 0, 0, 0);
@@ -589,10 +618,6 @@ __device__ __forceinline__ void coupling_gemm_xl_bf16x3(const float* __restrict_
             acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x1, q3[d][t], acc[t], 0, 0, 0);
             acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x2, q2[d][t], acc[t], 0, 0, 0);
             acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x3, q1[d][t], acc[t], 0, 0, 0);
-        }
-        const int kn = kg0 + kb + XD < NB ? kg0 + kb + XD : NB - 1;
-#pragma unroll
-        for (int t = 0; t < TPW; ++t) {
             q1[d][t] = ld(t, kn, 0);
             q2[d][t] = ld(t, kn, 1);
             q3[d][t] = ld(t, kn, 2);
@@ -600,35 +625,30 @@ __device__ __forceinline__ void coupling_gemm_xl_bf16x3(const float* __restrict_
     };
 #pragma unroll 1
     for (int c = 0; c < nchunk; ++c) {
-        const floatx4* xs4 = reinterpret_cast<const floatx4*>(Xs + (c & 1) * XL_CIMG + (lane >> 5) * XS_HALF +
-                                                              (lane & 31) * 4);
-        const int kg0 = c * KPC;
+        const bf16x8* xb = xsb + (c & 1) * CB + lane;
+        const int kg0 = c * NBC;
         const bool more = c + 1 < nchunk;
-        an0 = xs4[0];
-        an1 = xs4[XS_BLOCK / 4];
-        floatx4 nx[CPT];
+        n1 = xb[0];
+        n2 = xb[64];
+        n3 = xb[128];
+        floatx4 nx[NX];
 #pragma unroll
         for (int kb = 0; kb < PRE; ++kb) {
-            kblock(xs4, kg0, kb, kb % XD);
-            const int k = threadIdx.x + kb * NTHREADS;
-            if (kb < CPT && more && k < C4) nx[kb] = xg4[(size_t)(c + 1) * C4 + k];
+            kblock(xb, kg0, kb, kb % XD);
+            if (kb < NX && more) nx[kb] = xg4[src(c + 1, threadIdx.x + (kb >> 1) * NTHREADS, kb & 1)];
             __builtin_amdgcn_sched_barrier(0);
         }
 #pragma unroll 1
-        for (int kb = PRE; kb < KPC; kb += XD) {
+        for (int kb = PRE; kb < NBC; kb += XD) {
 #pragma unroll
             for (int d = 0; d < XD; ++d) {
-                kblock(xs4, kg0, kb + d, d);
+                kblock(xb, kg0, kb + d, d);
                 __builtin_amdgcn_sched_barrier(0);
             }
         }
-        if (more) {
-            floatx4* dst = (floatx4*)(Xs + ((c + 1) & 1) * XL_CIMG);
+        if (more) {  // the other buffer was last read in chunk c-1, before the previous barrier
 #pragma unroll
-            for (int u = 0; u < CPT; ++u) {
-                const int k = threadIdx.x + u * NTHREADS;
-                if (k < C4) dst[k] = nx[u];
-            }
+            for (int u = 0; u < PPT; ++u) put((c + 1) & 1, threadIdx.x + u * NTHREADS, nx[2 * u], nx[2 * u + 1]);
         }
         STAMP(2);
         lds_barrier();
