@@ -43,3 +43,20 @@ def test_records_hold_the_gate():
         else:
             assert R["s1000_t"].min() > 200.0 + 800.0   # the transient + 1000 steps of 0.80-0.90 units
             np.testing.assert_array_equal(R["s1000_step"], 1000)
+
+
+def test_stress_records_hold_three_steps():
+    """The N=8192 BF16X3 records (tests/golden/make_stress_fixtures.py):
+    reset + 3 steps of the sampled envs, clocks advancing, every env's step
+    counter at 3 and finite rewards (the GPU replay is
+    tests/test_gpu_stress.py)."""
+    import stress_scenarios as ss
+    for name, (envs, idx) in ss.SCENARIOS.items():
+        R = np.load(os.path.join(GOLDEN, f"stress_{name}.npz"))
+        assert str(R["coupling"]) == "bf16x3"
+        np.testing.assert_array_equal(R["idx"], idx)
+        assert int(R["part_osc"]) == (1024 if envs == 1024 else 256)
+        assert R["reset_y"].shape == (len(idx), 20)
+        np.testing.assert_array_equal(R[f"s{ss.STEPS}_step"], ss.STEPS)
+        assert np.all(R[f"s{ss.STEPS}_t"] > R["reset_t"])
+        assert all(np.all(np.isfinite(R[f"s{k}_reward"])) for k in range(1, ss.STEPS + 1))

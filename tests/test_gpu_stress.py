@@ -87,3 +87,42 @@ def test_stress_n8192_full_size_sampled(torch_gpu, envs, idx):
     assert not (sim.stats()[3] & 16)
     o.close()
     sim.close()
+
+
+@pytest.mark.parametrize("name", ["weak", "strong"])
+def test_stress_n8192_bf16x3_against_records(torch_gpu, name):
+    """The same two forms in the BF16X3 coupling (the split-group bf16x3
+    GEMMs: per-k-block split at parts of 1024, staged split with alpha split
+    in registers at parts of 256), replayed against the CPU oracle's records
+    committed by tests/golden/make_stress_fixtures.py (the split oracle at
+    N=8192 takes ~15 CPU-minutes per form, too long for the GPU box)."""
+    import stress_scenarios as ss
+    path = os.path.join(ROOT, "tests", "golden", f"stress_{name}.npz")
+    if not os.path.exists(path):
+        pytest.skip(f"{path} not generated")
+    R = np.load(path)
+    assert str(R["coupling"]) == "bf16x3"
+    torch = torch_gpu
+    sim_mod = importlib.import_module("dbs-gym_amd.sim")
+    cfg, alpha, omega, g_s, g_r, th0, ct, st, gain = ss.shard(name)
+    assert cfg.part_osc == int(R["part_osc"])
+    idx = R["idx"]
+    sim = sim_mod.KuraSim(cfg, 0)
+    sim.set_coupling(alpha)
+    sim.set_env_params(omega, g_s, g_r)
+    sim.set_env_gain(gain)
+    sim.set_spectral(ct, st)
+    obs = sim.reset(torch.from_numpy(th0), check_errors=True).cpu().numpy()
+    assert not (sim.stats()[3] & 16), "group barrier timed out"
+
+    def check(tag, rec):
+        for k, v in rec.items():
+            assert np.array_equal(v, R[f"{tag}_{k}"]), f"{tag}: {k} differs for envs {idx}"
+
+    check("reset", ss.snapshot(sim.get_state(), {"obs": obs}, idx))
+    for k in range(ss.STEPS):
+        sim.step(torch.from_numpy(ss.actions(name, k, cfg.n_elec)), check_errors=True)
+        outs = {key: getattr(sim, key).cpu().numpy() for key in ss.OUT_BIG + ss.OUT_SMALL}
+        check(f"s{k + 1}", ss.snapshot(sim.get_state(), outs, idx))
+    assert not (sim.stats()[3] & 16)
+    sim.close()
