@@ -174,7 +174,15 @@ __shared__ double s_smp_r[E_WG][KURA_S_MAX + 2];
 #ifndef KURA_XL_DEPTH4
 #define KURA_XL_DEPTH4 4
 #endif
-// ... and of its bf16x3 form, in 16-deep k-blocks (12 VGPRs per tile each)
+// split groups in BF16X3: parts of up to KURA_XL_SP_STAGED_MAXTPW * 256
+// oscillators stage the split operand and split alpha in registers
+// (coupling_gemm_xl_bf16x3); larger parts split per k-block with pre-split,
+// deduplicated alpha (coupling_gemm_xl_bf16x3_kb); same-box A/B,
+// profiles/r05_dedup_and_xl_forms_ab.txt
+#ifndef KURA_XL_SP_STAGED_MAXTPW
+#define KURA_XL_SP_STAGED_MAXTPW 1
+#endif
+// ... and the alpha ring of the bf16x3 forms, in 16-deep k-blocks (12 VGPRs per tile each)
 #ifndef KURA_XL_SP_DEPTH1
 #define KURA_XL_SP_DEPTH1 8
 #endif
@@ -521,11 +529,141 @@ __device__ __forceinline__ void coupling_gemm_xl(const float* __restrict__ xg, c
 }
 
 
-// The split-group GEMM in KURA_COUPLING_BF16X3: coupling_gemm_bf16x3's chain
-// (six part products per 16-deep k-block, k ascending over all NG
-// oscillators, so P/Q are the oracle's oracle_split_gemm_rows at any N),
-// with the pre-split alpha (split_alpha, full-N column tiles) of this
-// workgroup's TPW*256 columns through a ring of XD k-blocks per tile.  The
+// The split-group BF16X3 GEMM for parts of 512 and 1024 (TPW = 2, 4): the
+// sin/cos operand streamed in fp32 chunks of 512 as in coupling_gemm_xl and
+// split per k-block in every wave (shared by the wave's tiles), the
+// pre-split alpha fragments through a ring of XD 16-deep k-blocks per tile,
+// each fragment found through the image's offset map (the offsets of the
+// next refill read one k-block ahead).  At TPW >= 2 this beats the staged
+// split below (its chunks of 256 double the chunk barriers; same-box A/B,
+// profiles/r05_dedup_and_xl_forms_ab.txt).
+template <int TPW>
+__device__ __forceinline__ void coupling_gemm_xl_bf16x3_kb(const float* __restrict__ xg, const float* __restrict__ alpha_sw,
+                                                        float* Xs, int NG, int col0, floatx16 (&acc)[TPW],
+                                                        unsigned long long* dbg STAMP_PARAMS) {
+    (void)dbg;
+    NG = __builtin_amdgcn_readfirstlane(NG);
+    col0 = __builtin_amdgcn_readfirstlane(col0);
+    xg = uniform_ptr(xg);
+    const int NB = NG / 16;
+    const int NT = NG / 32;
+    constexpr int FRAG = 3 * 64 * 16;      // bytes per B fragment
+    const int nchunk = NG / XL_KC;
+    int lane;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+#pragma unroll
+    for (int t = 0; t < TPW; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[t][r] = 0.0f;
+    const float* au = uniform_ptr(alpha_sw);
+    // the deduplicated image (split_alpha_dedup: a map [NB][NT] of byte
+    // offsets, then the distinct fragments): at N = 8192 the 131072
+    // fragments of the reference's alpha are 992 distinct ones (3 MB)
+    const unsigned IMG = (unsigned)NT * NB * 4u + (unsigned)NT * NB * FRAG;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)au, 0, IMG, 0x00020000);
+    const float* mp = au + col0 / 32 + wave * TPW;          // map row b: mp[b * NT + t]
+    auto off = [&](int t, int b) -> int { return __builtin_bit_cast(int, mp[(size_t)b * NT + t]); };
+    auto ld = [&](int o, int p) -> bf16x8 {
+        KDBG_CHECK(dbg, o >= NT * NB * 4 && (unsigned)o + FRAG <= IMG);
+        return __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rs, (p * 64 + lane) * 16, o, 0));
+    };
+    constexpr int C4 = XL_CIMG / 4;
+    constexpr int CPT = (C4 + NTHREADS - 1) / NTHREADS;
+    gfloatx4* xg4 = (gfloatx4*)xg;
+    floatx4* xs4w = (floatx4*)Xs;
+    for (int k = threadIdx.x; k < C4; k += NTHREADS) xs4w[k] = xg4[k];
+    lds_barrier();
+    STAMP(18);
+    constexpr int XD = TPW >= 4 ? KURA_XL_SP_DEPTH4 : (TPW == 2 ? KURA_XL_SP_DEPTH2 : KURA_XL_SP_DEPTH1);
+    constexpr int KPC = XL_KC / 16;                // 16-deep k-blocks per chunk
+    constexpr int PRE = (CPT + XD - 1) / XD * XD;
+    static_assert(KPC % XD == 0 && PRE <= KPC, "alpha ring must tile the chunk");
+    bf16x8 q1[XD][TPW], q2[XD][TPW], q3[XD][TPW];
+    int om[TPW];   // fragment offsets of the next ring refill's k-block
+#pragma unroll
+    for (int d = 0; d < XD; ++d)
+#pragma unroll
+        for (int t = 0; t < TPW; ++t) {
+            const int o = off(t, d);
+            q1[d][t] = ld(o, 0);
+            q2[d][t] = ld(o, 1);
+            q3[d][t] = ld(o, 2);
+        }
+#pragma unroll
+    for (int t = 0; t < TPW; ++t) om[t] = off(t, XD < NB ? XD : NB - 1);
+    floatx4 an0, an1;   // the next k-block's two float4 of the operand (LDS, one block ahead)
+    auto kblock = [&](const floatx4* xs4, int kg0, int kb, int d) __attribute__((always_inline)) {
+        const floatx4 lo = an0, hi = an1;
+        const int nb = kb + 1 < KPC ? kb + 1 : KPC - 1;
+        an0 = xs4[(2 * nb) * (XS_BLOCK / 4)];
+        an1 = xs4[(2 * nb + 1) * (XS_BLOCK / 4)];
+        bf16x8 x1, x2, x3;
+        split_bf16x3(lo, hi, x1, x2, x3);
+#pragma unroll
+        for (int t = 0; t < TPW; ++t) {
+            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x1, q1[d][t], acc[t], 0, 0, 0);
+            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x1, q2[d][t], acc[t], 0, 0, 0);
+            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x2, q1[d][t], acc[t], 0, 0, 0);
+            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x1, q3[d][t], acc[t], 0, 0, 0);
+            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x2, q2[d][t], acc[t], 0, 0, 0);
+            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x3, q1[d][t], acc[t], 0, 0, 0);
+        }
+        const int kn1 = kg0 + kb + XD + 1 < NB ? kg0 + kb + XD + 1 : NB - 1;
+#pragma unroll
+        for (int t = 0; t < TPW; ++t) {
+            const int o = om[t];
+            q1[d][t] = ld(o, 0);
+            q2[d][t] = ld(o, 1);
+            q3[d][t] = ld(o, 2);
+            om[t] = off(t, kn1);
+        }
+    };
+#pragma unroll 1
+    for (int c = 0; c < nchunk; ++c) {
+        const floatx4* xs4 = reinterpret_cast<const floatx4*>(Xs + (c & 1) * XL_CIMG + (lane >> 5) * XS_HALF +
+                                                              (lane & 31) * 4);
+        const int kg0 = c * KPC;
+        const bool more = c + 1 < nchunk;
+        an0 = xs4[0];
+        an1 = xs4[XS_BLOCK / 4];
+        floatx4 nx[CPT];
+#pragma unroll
+        for (int kb = 0; kb < PRE; ++kb) {
+            kblock(xs4, kg0, kb, kb % XD);
+            const int k = threadIdx.x + kb * NTHREADS;
+            if (kb < CPT && more && k < C4) nx[kb] = xg4[(size_t)(c + 1) * C4 + k];
+            __builtin_amdgcn_sched_barrier(0);
+        }
+#pragma unroll 1
+        for (int kb = PRE; kb < KPC; kb += XD) {
+#pragma unroll
+            for (int d = 0; d < XD; ++d) {
+                kblock(xs4, kg0, kb + d, d);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+        if (more) {
+            floatx4* dst = (floatx4*)(Xs + ((c + 1) & 1) * XL_CIMG);
+#pragma unroll
+            for (int u = 0; u < CPT; ++u) {
+                const int k = threadIdx.x + u * NTHREADS;
+                if (k < C4) dst[k] = nx[u];
+            }
+        }
+        STAMP(2);
+        lds_barrier();
+        STAMP(17);
+    }
+}
+
+// The split-group GEMM in KURA_COUPLING_BF16X3 for parts of 256 (TPW = 1):
+// coupling_gemm_bf16x3's chain (six part products per 16-deep k-block, k
+// ascending over all NG oscillators, so P/Q are the oracle's
+// oracle_split_gemm_rows at any N).  alpha comes from the fp32 image
+// (swizzle_alpha) through a ring of XD k-blocks per tile and is split in
+// registers (4 bytes per element instead of 6: at one tile per wave the
+// CU's alpha fill rate, not VALU, bounds the loop).  The
 // sin/cos operand is split ONCE per chunk, while it is staged: each thread
 // loads the two float4 of (k-block, lane) pairs from the group image and
 // writes their three bf16 parts to LDS, so the k-block loop reads x1/x2/x3
@@ -542,7 +680,7 @@ __device__ __forceinline__ void coupling_gemm_xl_bf16x3(const float* __restrict_
     col0 = __builtin_amdgcn_readfirstlane(col0);
     xg = uniform_ptr(xg);
     const int NB = NG / 16;
-    const int TSTRIDE = NB * 3 * 64 * 16;   // bytes per column tile
+    const int TSTRIDE = NB * 2 * 64 * 16;   // bytes per column tile (the fp32 image)
     constexpr int KC = XL_KC_SP;
     constexpr int NBC = KC / 16;            // k-blocks per chunk
     constexpr int CB = NBC * 3 * 64;        // bf16x8 per chunk buffer
@@ -560,9 +698,9 @@ __device__ __forceinline__ void coupling_gemm_xl_bf16x3(const float* __restrict_
     const float* au = uniform_ptr(alpha_sw);
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
         (void*)((const char*)au + ((size_t)(col0 / 32) + wave * TPW) * TSTRIDE), 0, TPW * TSTRIDE, 0x00020000);
-    auto ld = [&](int t, int b, int p) -> bf16x8 {
-        KDBG_CHECK(dbg, b >= 0 && b < NB && ((b * 3 + p) * 64 + lane) * 16 + t * TSTRIDE + 16 <= TPW * TSTRIDE);
-        return __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rs, ((b * 3 + p) * 64 + lane) * 16,
+    auto ldf = [&](int t, int k) -> floatx4 {   // k8-block k of the fp32 image
+        KDBG_CHECK(dbg, k >= 0 && k < 2 * NB && (lane + k * 64) * 16 + t * TSTRIDE + 16 <= TPW * TSTRIDE);
+        return __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(rs, (lane + k * 64) * 16,
                                                                                  t * TSTRIDE, 0));
     };
     gfloatx4* xg4 = (gfloatx4*)xg;
@@ -593,14 +731,13 @@ __device__ __forceinline__ void coupling_gemm_xl_bf16x3(const float* __restrict_
     constexpr int NX = 2 * PPT;                    // staging loads per thread and chunk
     constexpr int PRE = (NX + XD - 1) / XD * XD;   // unrolled head: one staging load per k-block
     static_assert(NBC % XD == 0 && PRE <= NBC, "alpha ring must tile the chunk");
-    bf16x8 q1[XD][TPW], q2[XD][TPW], q3[XD][TPW];
+    floatx4 qlo[XD][TPW], qhi[XD][TPW];
 #pragma unroll
     for (int d = 0; d < XD; ++d)
 #pragma unroll
         for (int t = 0; t < TPW; ++t) {
-            q1[d][t] = ld(t, d, 0);
-            q2[d][t] = ld(t, d, 1);
-            q3[d][t] = ld(t, d, 2);
+            qlo[d][t] = ldf(t, 2 * d);
+            qhi[d][t] = ldf(t, 2 * d + 1);
         }
     bf16x8 n1, n2, n3;   // the next k-block's operand parts (LDS, one block ahead)
     auto kblock = [&](const bf16x8* xb, int kg0, int kb, int d) __attribute__((always_inline)) {
@@ -612,15 +749,16 @@ __device__ __forceinline__ void coupling_gemm_xl_bf16x3(const float* __restrict_
         const int kn = kg0 + kb + XD < NB ? kg0 + kb + XD : NB - 1;
 #pragma unroll
         for (int t = 0; t < TPW; ++t) {
-            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x1, q1[d][t], acc[t], 0, 0, 0);
-            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x1, q2[d][t], acc[t], 0, 0, 0);
-            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x2, q1[d][t], acc[t], 0, 0, 0);
-            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x1, q3[d][t], acc[t], 0, 0, 0);
-            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x2, q2[d][t], acc[t], 0, 0, 0);
-            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x3, q1[d][t], acc[t], 0, 0, 0);
-            q1[d][t] = ld(t, kn, 0);
-            q2[d][t] = ld(t, kn, 1);
-            q3[d][t] = ld(t, kn, 2);
+            bf16x8 a1, a2, a3;
+            split_bf16x3(qlo[d][t], qhi[d][t], a1, a2, a3);
+            qlo[d][t] = ldf(t, 2 * kn);
+            qhi[d][t] = ldf(t, 2 * kn + 1);
+            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x1, a1, acc[t], 0, 0, 0);
+            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x1, a2, acc[t], 0, 0, 0);
+            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x2, a1, acc[t], 0, 0, 0);
+            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x1, a3, acc[t], 0, 0, 0);
+            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x2, a2, acc[t], 0, 0, 0);
+            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x3, a1, acc[t], 0, 0, 0);
         }
     };
 #pragma unroll 1
@@ -1832,13 +1970,17 @@ __device__ KURA_SOLVE_ATTR void solve_wg(DevParamsK& __restrict__ pin, float* Xs
             const float* xgrp = uniform_ptr(group_publish_x<TPW>(p, pt, Xs));   // all parts' images of this stage
             xown = xgrp + (size_t)__builtin_amdgcn_readfirstlane(pt.part) * xl_img(TPW);
             STAMP(16);  // split groups: image publish + group barrier (slot 16 is free outside KURA_STAMPS_SI)
-            if constexpr (SP)
+            if constexpr (SP) {
 #ifdef KURA_DEBUG
-                coupling_gemm_xl_bf16x3<TPW>(xgrp, p.alpha_sw, Xs, NG, col0, acc, uniform_ptr(p.stats) STAMP_ARGS);
+                unsigned long long* dbg = uniform_ptr(p.stats);
 #else
-                coupling_gemm_xl_bf16x3<TPW>(xgrp, p.alpha_sw, Xs, NG, col0, acc, nullptr STAMP_ARGS);
+                unsigned long long* dbg = nullptr;
 #endif
-            else
+                if constexpr (TPW > KURA_XL_SP_STAGED_MAXTPW)
+                    coupling_gemm_xl_bf16x3_kb<TPW>(xgrp, p.alpha_sw, Xs, NG, col0, acc, dbg STAMP_ARGS);
+                else
+                    coupling_gemm_xl_bf16x3<TPW>(xgrp, p.alpha_sw, Xs, NG, col0, acc, dbg STAMP_ARGS);
+            } else
                 coupling_gemm_xl<TPW>(xgrp, p.alpha_sw, Xs, NG, col0, acc STAMP_ARGS);
         } else {
 #ifdef KURA_DEBUG
