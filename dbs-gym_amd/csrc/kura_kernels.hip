@@ -294,33 +294,42 @@ __device__ __forceinline__ void coupling_gemm_bf16x3(const float* __restrict__ X
         return __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rs, ((b * 3 + p) * 64 + lane) * 16,
                                                                                  t * TSTRIDE, 0));
     };
-    bf16x8 a1[TPW], a2[TPW], a3[TPW];
+    // two register sets per tile: block b+2's parts load right after block
+    // b's MFMAs, a whole block of cover (one set: the loads issue after the
+    // block's last x3*a1 and the next block's first MFMA waits on them;
+    // +2 % on the step, profiles/r05_k1_ring2_ab.txt)
+    bf16x8 a1[2][TPW], a2[2][TPW], a3[2][TPW];
 #pragma unroll
-    for (int t = 0; t < TPW; ++t) {
-        a1[t] = ld(t, 0, 0);
-        a2[t] = ld(t, 0, 1);
-        a3[t] = ld(t, 0, 2);
-    }
-    // one register set per tile, refilled with the next k-block right after
-    // its six MFMAs (cover: the other tiles' MFMAs and the partner wave's)
-#pragma unroll 1
-    for (int b = 0; b < NB; ++b) {
-        bf16x8 x1, x2, x3;
-        split_bf16x3(xs4[(2 * b) * (XS_BLOCK / 4)], xs4[(2 * b + 1) * (XS_BLOCK / 4)], x1, x2, x3);
-        const int bn = b + 1 < NB ? b + 1 : NB - 1;
+    for (int d = 0; d < 2; ++d)
 #pragma unroll
         for (int t = 0; t < TPW; ++t) {
-            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x1, a1[t], acc[t], 0, 0, 0);
-            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x1, a2[t], acc[t], 0, 0, 0);
-            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x2, a1[t], acc[t], 0, 0, 0);
-            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x1, a3[t], acc[t], 0, 0, 0);
-            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x2, a2[t], acc[t], 0, 0, 0);
-            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x3, a1[t], acc[t], 0, 0, 0);
-            a1[t] = ld(t, bn, 0);
-            a2[t] = ld(t, bn, 1);
-            a3[t] = ld(t, bn, 2);
+            a1[d][t] = ld(t, d < NB ? d : NB - 1, 0);
+            a2[d][t] = ld(t, d < NB ? d : NB - 1, 1);
+            a3[d][t] = ld(t, d < NB ? d : NB - 1, 2);
+        }
+    auto blk = [&](int b, int d) __attribute__((always_inline)) {
+        bf16x8 x1, x2, x3;
+        split_bf16x3(xs4[(2 * b) * (XS_BLOCK / 4)], xs4[(2 * b + 1) * (XS_BLOCK / 4)], x1, x2, x3);
+        const int bn = b + 2 < NB ? b + 2 : NB - 1;
+#pragma unroll
+        for (int t = 0; t < TPW; ++t) {
+            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x1, a1[d][t], acc[t], 0, 0, 0);
+            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x1, a2[d][t], acc[t], 0, 0, 0);
+            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x2, a1[d][t], acc[t], 0, 0, 0);
+            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x1, a3[d][t], acc[t], 0, 0, 0);
+            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x2, a2[d][t], acc[t], 0, 0, 0);
+            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x3, a1[d][t], acc[t], 0, 0, 0);
+            a1[d][t] = ld(t, bn, 0);
+            a2[d][t] = ld(t, bn, 1);
+            a3[d][t] = ld(t, bn, 2);
         }
         __builtin_amdgcn_sched_barrier(0);
+    };
+    static_assert(NB % 2 == 0, "two-block ring");
+#pragma unroll 1
+    for (int b = 0; b < NB; b += 2) {
+        blk(b, 0);
+        blk(b + 1, 1);
     }
 }
 
