@@ -142,6 +142,7 @@ _SYMBOLS = {
     "kura_get_stats": (c_int, [c_void_p, c_void_p, c_int]),
     "kura_get_env_flags": (c_int, [c_void_p, c_void_p, c_void_p]),
     "kura_set_row_capture": (c_int, [c_void_p, c_void_p]),
+    "kura_set_transient_capture": (c_int, [c_void_p, c_void_p]),
     "kura_get_stamps": (c_int, [c_void_p, c_void_p]),
     "kura_selftest_math": (c_int, [c_void_p, c_void_p, c_void_p, c_int]),
     "kura_selftest_gemm": (c_int, [c_void_p, c_void_p, c_void_p, c_int]),

@@ -99,6 +99,8 @@ struct DevParams {
     int* ep_len;            // [B] samples appended since the env's last reset
     int* eflags;            // [B] per-env failure bits of the last launch (KURA_F_*, kura.h), 0 = ok
     float* rows;            // optional [B][KURA_S_MAX+1][N]: every saved row of a step (sol_state_, env.py:430,440)
+    double* lfp_tr;         // optional [B][n_transient - 1]: the LFP of every transient row of a reset but the
+                            // last (theta_record_transient, env.py:611); NULL: only the last W rows are evaluated
     float* gemm_dump;       // KURA_DEBUG builds: [sweep][2][32][N] operand and coupling sums of workgroup 0
     int gemm_dump_n;        // ... sweeps to keep (kura_debug_gemm_dump)
 };
@@ -1709,9 +1711,16 @@ __device__ __forceinline__ void save_pass(DevParamsK& __restrict__ p, const Slot
                 const float ln = rm_total(e, k) / (float)NG;
                 const double lr = gauss ? 0.0 + rm_total_d(e, k) / (double)NG : (double)ln;
                 const int pos = c.sv_si + r0 + k - c.lfp_from + c.pos0;
-                KDBG_CHECK(p.stats, pos >= 0 && (to_ring ? pos < p.W : pos < KURA_S_MAX + 2) && env_base + e < p.B);
+                KDBG_CHECK(p.stats, pos >= 0 && (to_ring ? pos < (p.lfp_tr ? c.n - 1 : p.W) : pos < KURA_S_MAX + 2) &&
+                                        env_base + e < p.B);
                 if (to_ring) {
-                    p.ring[(size_t)(env_base + e) * p.W + pos] = lr;
+                    // (reset: with the transient record on, every row feeds a sample and the ring takes the last W)
+                    int rp = pos;
+                    if (p.lfp_tr) {
+                        p.lfp_tr[(size_t)(env_base + e) * (c.n - 1) + pos] = lr;
+                        rp = pos - (c.n - 1 - p.W);
+                    }
+                    if (rp >= 0) p.ring[(size_t)(env_base + e) * p.W + rp] = lr;
                 } else {
                     s_smp_n[e][pos] = ln;
                     s_smp_r[e][pos] = lr;
@@ -1739,10 +1748,16 @@ __device__ __forceinline__ void save_pass(DevParamsK& __restrict__ p, const Slot
                 const float ln = ltot[k] / (float)NG;
                 const double lr = gauss ? 0.0 + ltot_d[k] / (double)NG : (double)ln;
                 const int pos = si - c.lfp_from + c.pos0;
-                KDBG_CHECK(p.stats, pos >= 0 && (to_ring ? pos < p.W : pos < KURA_S_MAX + 2) && env_base + tid < p.B);
-                if (to_ring) {
-                    if (pt.part == 0) p.ring[(size_t)(env_base + tid) * p.W + pos] = lr;
-                } else {
+                KDBG_CHECK(p.stats, pos >= 0 && (to_ring ? pos < (p.lfp_tr ? c.n - 1 : p.W) : pos < KURA_S_MAX + 2) &&
+                                        env_base + tid < p.B);
+                if (to_ring && pt.part == 0) {
+                    int rp = pos;
+                    if (p.lfp_tr) {
+                        p.lfp_tr[(size_t)(env_base + tid) * (c.n - 1) + pos] = lr;
+                        rp = pos - (c.n - 1 - p.W);
+                    }
+                    if (rp >= 0) p.ring[(size_t)(env_base + tid) * p.W + rp] = lr;
+                } else if (!to_ring) {
                     s_smp_n[tid][pos] = ln;
                     s_smp_r[tid][pos] = lr;
                 }
@@ -2537,7 +2552,7 @@ __device__ __forceinline__ void reset_pair(DevParamsK& p, Part& pt, float* Xs, c
         const int env = env_base + tid;
         if (env < p.B && (!mask || mask[env])) {
             const Grid g = make_grid(0.0, p.transient_len, p.dt);
-            ctl_begin(s_ctl[tid], g, p.dt0, g.n - 1 - W, g.n - 1, 0);
+            ctl_begin(s_ctl[tid], g, p.dt0, p.lfp_tr ? 0 : g.n - 1 - W, g.n - 1, 0);
         }
     }
     // state y <- theta0 for the masked envs

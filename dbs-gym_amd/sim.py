@@ -202,6 +202,21 @@ class KuraSim:
             check(self.lib, self.lib.kura_set_row_capture(self._h, None), "kura_set_row_capture")
             self.rows = None
 
+    def capture_transient(self, on: bool = True) -> None:
+        """Keep theta_record_transient (env.py:611) of every reset in
+        ``self.lfp_transient`` (B, T-1) float64: the LFP of each transient row
+        but the last, T = len(np.arange(0, transient_state_len, verbose_dt));
+        its last W columns are the reset's observation window.  Costs the LFP
+        of T-1-W more rows per reset (kura_set_transient_capture)."""
+        if on:
+            T = len(np.arange(0.0, self.cfg.transient_len, self.cfg.dt))
+            self.lfp_transient = torch.zeros((self.B, T - 1), dtype=torch.float64, device=self.device)
+            check(self.lib, self.lib.kura_set_transient_capture(self._h, ptr(self.lfp_transient)),
+                  "kura_set_transient_capture")
+        else:
+            check(self.lib, self.lib.kura_set_transient_capture(self._h, None), "kura_set_transient_capture")
+            self.lfp_transient = None
+
     def failed_envs(self, mask: torch.Tensor | None = None):
         """(env indices, KURA_F_* bits) of the envs whose last launch failed (synchronises)."""
         f = self.flags.cpu().numpy()

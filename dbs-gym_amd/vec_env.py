@@ -562,6 +562,13 @@ class KuraVectorEnv:
             return [self.np_random[i] for i in idx]
         if name == "init_state":                                    # env.py:594-598 (float64 draws)
             return [self._theta0[i].copy() for i in idx]
+        if name == "theta_record_transient":                        # env.py:611
+            tr = getattr(self.sim, "lfp_transient", None)
+            if tr is None:
+                raise AttributeError(_UNSERVED[name])
+            v = tr.cpu().numpy()
+            naive = self.sim.cfg.rec_kernel == 0
+            return [v[i].astype(np.float32) if naive else v[i].copy() for i in idx]
         if name in _UNSERVED:
             raise AttributeError(_UNSERVED[name])
         raise AttributeError(name)
@@ -656,10 +663,10 @@ _SOL_STATE_AFTER_RESET = ("sol_state after reset() would be the transient's 4000
 # reference attributes the GPU path does not keep (no caller in the reference
 # reads them: aDBS_RL/, the notebooks); asking for them raises with the reason
 _UNSERVED = {
-    "theta_record_transient": "theta_record_transient (env.py:611: the LFP of all 3999 transient rows) is not kept: "
-                              "the reset kernel forms only the last W samples, the observation window "
-                              "(theta_state / the reset's obs); the first 3999 - W rows feed no output and are "
-                              "not evaluated (DESIGN.md section 5, K2)",
+    "theta_record_transient": "theta_record_transient (env.py:611: the LFP of all 3999 transient rows) is kept only "
+                              "on request: call venv.sim.capture_transient(True) before reset() (SpatialKuramoto "
+                              "does); otherwise the reset kernel forms only the last W samples, the observation "
+                              "window (DESIGN.md section 5, K2)",
 }
 
 
@@ -676,6 +683,7 @@ class SpatialKuramoto:
         self._v = KuraVectorEnv([params_dict], device=device, rand_seeds=[params_dict["rand_seed"]],
                                 autoreset=False, failure_check="eager")
         self._v.sim.capture_rows(True)          # sol_state_: every row of the step (env.py:430,440)
+        self._v.sim.capture_transient(True)     # theta_record_transient (env.py:611)
         self.action_space = self._v.single_action_space
         self.observation_space = self._v.single_observation_space
         self.current_step = 0
@@ -762,7 +770,8 @@ class SpatialKuramoto:
 
     @property
     def theta_record_transient(self):
-        raise AttributeError(_UNSERVED["theta_record_transient"])
+        """calc_lfp(sol_state[:-1]) of the last reset's transient (env.py:611): (T-1,)"""
+        return self._v.get_attr("theta_record_transient")[0]
 
     def _reward(self, kind, x_state, action_value):
         """Any 1-D length (the bins follow len(x_state), utils.py:21-27)."""

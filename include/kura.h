@@ -267,6 +267,15 @@ int kura_debug_gemm_dump(KuraHandle* h, float* dev_buf, int n);
  * store per saved value; off by default. */
 int kura_set_row_capture(KuraHandle* h, float* rows_dev);
 
+/* optional record of a reset's transient (env.py:610-611,
+ * theta_record_transient = calc_lfp(sol_state[:-1])): lfp_dev (device,
+ * B*(T-1) float64 with T = len(np.arange(0, transient_state_len,
+ * verbose_dt)), or NULL to stop) receives, for each env a kura_reset
+ * resets, the LFP of every transient row but the last (the last W of them
+ * are the observation window).  Costs the LFP of T-1-W more rows per
+ * reset; off by default. */
+int kura_set_transient_capture(KuraHandle* h, double* lfp_dev);
+
 /* per-env KURA_F_* bits of the last kura_step / kura_reset (0 = ok), copied
  * into the caller's device buffer out_dev (B int32) on the given stream:
  * read them with the step's outputs (no extra synchronisation). */

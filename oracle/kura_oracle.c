@@ -644,10 +644,12 @@ static double rescale_action(const KuraConfig* c, float a) {
 }
 
 /* reset(): transient solve from theta0 over arange(0, transient_len, dt);
- * window = last W of LFP(rows[:-1]).  Arrays are B-major. */
-int oracle_reset(void* ctx, int B, const float* omega, const double* g_rec, const float* theta0, float* y,
-                 double* t, int32_t* step, double* ring, int32_t* wpos, float* obs, int64_t* stats_out,
-                 int32_t* eflags, const double* ctab, const double* stab, double* spec) {
+ * window = last W of LFP(rows[:-1]) (env.py:606-612).  Arrays are B-major.
+ * lfp_tr (B * (T-1), or NULL): theta_record_transient, the LFP of every
+ * transient row but the last (env.py:611; kura_set_transient_capture). */
+int oracle_reset_ex(void* ctx, int B, const float* omega, const double* g_rec, const float* theta0, float* y,
+                    double* t, int32_t* step, double* ring, int32_t* wpos, float* obs, int64_t* stats_out,
+                    int32_t* eflags, const double* ctab, const double* stab, double* spec, double* lfp_tr) {
     OCtx* o = (OCtx*)ctx;
     const KuraConfig* cfg = &o->cfg;
     const int N = o->N, W = cfg->window;
@@ -656,8 +658,10 @@ int oracle_reset(void* ctx, int B, const float* omega, const double* g_rec, cons
 #pragma omp parallel reduction(| : rc)
     {
         Work w;
-        float* lf = (float*)malloc(sizeof(float) * W);
-        double* lr = (double*)malloc(sizeof(double) * W);
+        const Grid g0 = arange(0.0, cfg->transient_len, cfg->dt);
+        const int nl = lfp_tr ? g0.n - 1 : W;     /* LFP rows evaluated: all, or the window's */
+        float* lf = (float*)malloc(sizeof(float) * nl);
+        double* lr = (double*)malloc(sizeof(double) * nl);
         if (work_alloc(&w, N) || !lf || !lr) rc |= 1;
 #pragma omp for schedule(dynamic, 1)
         for (int b = 0; b < B; ++b) {
@@ -667,15 +671,16 @@ int oracle_reset(void* ctx, int B, const float* omega, const double* g_rec, cons
             memcpy(yb, theta0 + (size_t)b * N, sizeof(float) * N);
             w.kn = kn_of(o, b);
             Stats st = {0, 0, 0, 0};
-            Sink sk = {NULL, lf, lr, g.n - 1 - W, g.n - 1, g_rec + (size_t)b * cfg->n_rec * N};
+            Sink sk = {NULL, lf, lr, g.n - 1 - nl, g.n - 1, g_rec + (size_t)b * cfg->n_rec * N};
             solve(o, &w, &g, yb, omega + (size_t)b * N, w.zero, &sk, &st);
             t[b] = grid_at(&g, g.n - 1);
             step[b] = 0;
-            for (int i = 0; i < W; ++i) ring[(size_t)b * W + i] = lr[i];
+            if (lfp_tr) memcpy(lfp_tr + (size_t)b * nl, lr, sizeof(double) * nl);
+            for (int i = 0; i < W; ++i) ring[(size_t)b * W + i] = lr[nl - W + i];
             wpos[b] = 0;
             if (eflags) eflags[b] = (int32_t)st.flags;
             if (obs)
-                for (int i = 0; i < W; ++i) obs[(size_t)b * W + i] = (float)lr[i];
+                for (int i = 0; i < W; ++i) obs[(size_t)b * W + i] = (float)lr[nl - W + i];
             if (spec && cfg->reward_kind != KURA_R_TEMP_CONST)
                 spec_init(cfg, ring + (size_t)b * W, ctab, stab, spec + (size_t)b * 2 * cfg->n_bins);
 #pragma omp critical
@@ -692,6 +697,13 @@ int oracle_reset(void* ctx, int B, const float* omega, const double* g_rec, cons
     }
     if (stats_out) memcpy(stats_out, agg, sizeof(agg));
     return rc ? KURA_E_NOMEM : KURA_OK;
+}
+
+int oracle_reset(void* ctx, int B, const float* omega, const double* g_rec, const float* theta0, float* y,
+                 double* t, int32_t* step, double* ring, int32_t* wpos, float* obs, int64_t* stats_out,
+                 int32_t* eflags, const double* ctab, const double* stab, double* spec) {
+    return oracle_reset_ex(ctx, B, omega, g_rec, theta0, y, t, step, ring, wpos, obs, stats_out, eflags, ctab, stab,
+                           spec, NULL);
 }
 
 /* step(): env.py:415-454 for B envs.  State arrays (y, t, step, ring, wpos)

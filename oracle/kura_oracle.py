@@ -40,6 +40,8 @@ def lib() -> ctypes.CDLL:
         L.oracle_destroy.argtypes = [c_void_p]
         L.oracle_reset.restype = c_int
         L.oracle_reset.argtypes = [c_void_p, c_int] + [c_void_p] * 14
+        L.oracle_reset_ex.restype = c_int
+        L.oracle_reset_ex.argtypes = [c_void_p, c_int] + [c_void_p] * 15
         L.oracle_step.restype = c_int
         L.oracle_step.argtypes = [c_void_p, c_int] + [c_void_p] * 20
         L.oracle_spec_init.argtypes = [c_void_p, c_int] + [c_void_p] * 4
@@ -120,15 +122,20 @@ class Oracle:
         self.ctab = np.ascontiguousarray(ctab, np.float64)
         self.stab = np.ascontiguousarray(stab, np.float64)
 
-    def reset(self, theta0):
+    def reset(self, theta0, transient=False):
+        """oracle_reset; transient=True also returns theta_record_transient
+        (B, T-1) float64, the LFP of every transient row but the last
+        (env.py:611, oracle_reset_ex)."""
         th = np.ascontiguousarray(theta0, np.float32)
         obs = np.zeros((self.B, self.W), np.float32)
-        rc = lib().oracle_reset(self._ctx, self.B, _p(self.omega), _p(self.g_rec), _p(th), _p(self.y), _p(self.t),
-                                _p(self.step_count), _p(self.ring), _p(self.wpos), _p(obs), _p(self.stats),
-                                _p(self.flags), _p(getattr(self, "ctab", None)), _p(getattr(self, "stab", None)),
-                                _p(self.spec) if hasattr(self, "ctab") else None)
+        T = len(arange(0.0, self.cfg.transient_len, self.cfg.dt))
+        tr = np.zeros((self.B, T - 1), np.float64) if transient else None
+        rc = lib().oracle_reset_ex(self._ctx, self.B, _p(self.omega), _p(self.g_rec), _p(th), _p(self.y), _p(self.t),
+                                   _p(self.step_count), _p(self.ring), _p(self.wpos), _p(obs), _p(self.stats),
+                                   _p(self.flags), _p(getattr(self, "ctab", None)), _p(getattr(self, "stab", None)),
+                                   _p(self.spec) if hasattr(self, "ctab") else None, _p(tr))
         assert rc == 0
-        return obs
+        return (obs, tr) if transient else obs
 
     def step(self, action):
         a = np.ascontiguousarray(action, np.float32)

@@ -58,6 +58,9 @@ def test_single_env_sol_state_rows():
     assert not np.array_equal(th0, env.init_state)
     with pytest.raises(AttributeError, match="transient"):
         env.sol_state
-    with pytest.raises(AttributeError, match="3999"):
-        env.theta_record_transient
+    # theta_record_transient (env.py:611): the LFP of the 3999 transient rows,
+    # whose last W are the observation the reset returned
+    tr = env.theta_record_transient
+    assert tr.shape == (3999,)
+    np.testing.assert_array_equal(tr[-env._v.W:].astype(np.float32), env.theta_state.ravel())
     env.close()
