@@ -1663,6 +1663,13 @@ __device__ __forceinline__ void save_pass(DevParamsK& __restrict__ p, const Slot
 #pragma unroll
             for (int q = 0; q < 8; ++q) {
                 const int f = fl[q] >> (3 * k);
+                // recorder LFP: an empty slot (no sample, not the state, not
+                // captured) skips its dense output, cos and f64 partial --
+                // the reset's lockstep passes have many (-20 % on the env1
+                // reset); for the naive LFP the branch costs more than it
+                // saves (profiles/r05_save_skip_ab.txt)
+                v[q] = 0.0f;
+                if (gauss && !(f & (capture ? 7 : 6))) continue;
                 const float x = th[k][q];
                 float w = ca[q] * x + cb[q];
                 w = w * x + cc[q];
