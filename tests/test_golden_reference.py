@@ -207,3 +207,26 @@ def test_trajectory_through_reference_plumbing(tag, reward, coupling):
         np.testing.assert_allclose(out["lfp_true"][0, :S], G[f"traj_{tag}_theta_mean"][k, :S], rtol=0, atol=1e-6)
         assert not np.any(G[f"traj_{tag}_theta_mean"][k, S:])
         assert out["reward"][0] == pytest.approx(G[f"traj_{tag}_rew"][k], rel=1e-4, abs=1e-7)
+
+
+G8 = np.load(os.path.join(os.path.dirname(__file__), "golden", "reference_r05_n8192.npz"))
+
+
+@pytest.mark.parametrize("coupling", COUPLINGS)
+def test_rhs_matches_reference_op_sequence_n8192(coupling):
+    """The same pin at the N = 8192 stress size (BASELINE configs[4], the
+    32x16x16 grid; tests/golden/make_golden_r05_n8192.py): the reference's
+    own RHS on two states with phases up to 6e3 rad and one in [0, 2pi).  The
+    oracle's alpha is rebuilt from the coordinates and must hash to the
+    reference's.  Measured max |diff| 4.8e-7 in both arithmetics (F32 and
+    BF16X3 alike), so AUTO = BF16X3 holds the reference pin at every N."""
+    alpha = ms.coupling_alpha(G8["rhs_n8192_coords"]).astype(np.float32)
+    assert hashlib.sha1(alpha.tobytes()).digest() == G8["rhs_n8192_alpha_sha1"].tobytes()
+    p = kura.synthetic_params("env0", 8192)
+    cfg = sim_mod.make_config(p, 1, reward_func="bbpow_action", coupling=coupling)
+    assert kura.coupling_of(cfg) == coupling
+    o = ko.Oracle(cfg, alpha)
+    for y, f_ref in zip(G8["rhs_n8192_y"], G8["rhs_n8192_f"]):
+        f = o.rhs(y, G8["rhs_n8192_w0"], G8["rhs_n8192_pulse"])
+        np.testing.assert_allclose(f, f_ref, rtol=0, atol=RHS_ATOL, err_msg=coupling)
+    o.close()
