@@ -60,7 +60,7 @@ def parse(argv=None):
                     help="--episode with episode_metrics=True (beta power + envelope of every finished episode)")
     ap.add_argument("--reward", default="bbpow_action")
     ap.add_argument("--coupling", default="auto", choices=["auto", "f32", "bf16x3"],
-                    help="coupling arithmetic (kura.h KURA_COUPLING_*; auto = bf16x3 for N <= 1024, f32 above)")
+                    help="coupling arithmetic (kura.h KURA_COUPLING_*; auto = bf16x3 at every N)")
     ap.add_argument("--cpu-seconds", type=float, default=24.0,
                     help="bounded CPU-baseline budget in seconds (0 = skip), split over its legs")
     ap.add_argument("--seed", type=int, default=2024)

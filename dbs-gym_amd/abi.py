@@ -42,7 +42,7 @@ REWARD_KINDS = {
     "temp_const_action": KURA_R_TEMP_CONST,
     "bbpow_threth_action": KURA_R_BBPOW_THR,
 }
-# coupling arithmetic (kura.h KURA_COUPLING_*): "auto" = bf16x3 for N <= 1024, f32 above
+# coupling arithmetic (kura.h KURA_COUPLING_*): "auto" = bf16x3 at every N
 KURA_COUPLING_AUTO = 0
 KURA_COUPLING_F32 = 1
 KURA_COUPLING_BF16X3 = 2
@@ -53,7 +53,7 @@ def coupling_of(cfg) -> str:
     """The arithmetic a config resolves to (kura.h kura_coupling_of)."""
     c = int(cfg.coupling)
     if c == KURA_COUPLING_AUTO:
-        c = KURA_COUPLING_BF16X3 if cfg.n_osc <= 1024 else KURA_COUPLING_F32
+        c = KURA_COUPLING_BF16X3
     return {KURA_COUPLING_F32: "f32", KURA_COUPLING_BF16X3: "bf16x3"}[c]
 
 

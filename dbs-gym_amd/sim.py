@@ -39,7 +39,7 @@ def make_config(params: dict, n_envs: int, reward_func: str | None = None, max_s
     picks one that fills the GPU).  coupling: the arithmetic of the O(N^2)
     coupling sums (kura.h KURA_COUPLING_*): "bf16x3" (three-way bf16 splits on
     the bf16 MFMA, fp32 accumulation), "f32" (fmaf chain on the fp32 MFMA) or
-    "auto" (bf16x3 for N <= 1024, f32 above); results depend on it bit for bit."""
+    "auto" (bf16x3 at every N); results depend on it bit for bit."""
     p = params
     step_len = p["electrode_width"] + p["electrode_pause"]                      # env.py:294
     wind_len = step_len * p["observe_wind_counts"]                               # env.py:296

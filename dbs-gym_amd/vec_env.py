@@ -96,7 +96,7 @@ class KuraVectorEnv:
                 terminated.
     coupling:   arithmetic of the O(N^2) coupling sums (kura.h
                 KURA_COUPLING_*, ``make_config``): "auto" (default; "bf16x3"
-                for N <= 1024, "f32" above), "bf16x3" or "f32".
+                at every N), "bf16x3" or "f32".
     """
 
     metadata = {"render.modes": ["human"]}

@@ -43,7 +43,7 @@ def test_debug_build_in_bounds_and_bit_exact(monkeypatch, name, n_osc, reward, m
         monkeypatch.setenv("KURA_XL_MAX_GRID", max_grid)
     sim_mod = importlib.import_module("dbs-gym_amd.sim")
     B = 20
-    cfg, alpha, omega, gs, gr, th0, ct, st, _ = make_case(name, n_osc, B, reward=reward)
+    cfg, alpha, omega, gs, gr, th0, ct, st, _ = make_case(name, n_osc, B, reward=reward, coupling="f32" if n_osc > 1024 else "auto")
     sim = sim_mod.KuraSim(cfg, 0, lib_path=DEBUG_LIB)
     sim.set_coupling(alpha)
     sim.set_env_params(omega, gs, gr)

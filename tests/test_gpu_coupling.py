@@ -56,14 +56,16 @@ def test_each_coupling_is_a_twin_and_they_differ(torch_gpu):
 
 
 def test_split_groups_take_either_coupling(torch_gpu):
-    """n_osc > 1024: AUTO is F32; an explicit BF16X3 request builds the
-    split-group bf16x3 kernels (parity: tests/test_gpu_split.py); an unknown
-    value is refused."""
+    """n_osc > 1024: AUTO is BF16X3 there too (the split-group bf16x3
+    kernels; parity: tests/test_gpu_split.py, tests/test_gpu_stress.py); an
+    explicit F32 request builds the F32 split-group kernels; an unknown value
+    is refused."""
     sim_mod = importlib.import_module("dbs-gym_amd.sim")
     cfg, *_ = make_case("env0", 2048, 2)
-    assert kura.coupling_of(cfg) == "f32"
-    cfg.coupling = kura.abi.KURA_COUPLING_BF16X3
     assert kura.coupling_of(cfg) == "bf16x3"
+    sim_mod.KuraSim(cfg, 0).close()
+    cfg.coupling = kura.abi.KURA_COUPLING_F32
+    assert kura.coupling_of(cfg) == "f32"
     sim_mod.KuraSim(cfg, 0).close()
     cfg.coupling = 7
     with pytest.raises(ValueError, match="coupling=7"):

@@ -26,7 +26,7 @@ DEBUG_LIB = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file_
                          "libkura_debug.so")
 
 
-def _pair(torch, N, B, steps, reward="bbpow_action", name="env0", gains=None, part=0, lib=None, coupling="auto"):
+def _pair(torch, N, B, steps, reward="bbpow_action", name="env0", gains=None, part=0, lib=None, coupling="f32"):
     sim_mod = importlib.import_module("dbs-gym_amd.sim")
     cfg, alpha, omega, gs, gr, th0, ct, st, _ = make_case(name, N, B, reward=reward, coupling=coupling)
     cfg.part_osc = part

@@ -57,7 +57,7 @@ def test_stress_n8192_full_size_sampled(torch_gpu, envs, idx):
     bench = _bench()
     sim_mod = importlib.import_module("dbs-gym_amd.sim")
     args = types.SimpleNamespace(config="env0", osc=8192, envs=envs, seed=2024, random_k=False,
-                                 reward="bbpow_action", part_osc=-1, coupling="auto")
+                                 reward="bbpow_action", part_osc=-1, coupling="f32")   # BF16X3 (AUTO): records below
     cfg, alpha, omega, g_s, g_r, th0, ct, st, gain = bench.build_shard(args, 0)
     assert cfg.part_osc == (1024 if envs == 1024 else 256)   # sim.auto_part_osc
     sim = sim_mod.KuraSim(cfg, 0)

@@ -21,8 +21,8 @@ tail -2 $O/gpu_tests.log; cat $O/smoke.log | tail -1
 [ "$2" = "quick" ] && { echo QUICKDONE; exit 0; }
 timeout -k 10 300 python3 bench.py --osc 8192 --envs 128 --steps 10 --warmup 2 --cpu-seconds 0 > $O/bench_stress128.json 2> $O/bench_stress128.err &&
 timeout -k 10 300 python3 bench.py --osc 8192 --envs 1024 --steps 4 --warmup 2 --cpu-seconds 0 > $O/bench_stress1024.json 2> $O/bench_stress1024.err &&
-timeout -k 10 300 python3 bench.py --osc 8192 --envs 128 --coupling bf16x3 --steps 10 --warmup 2 --cpu-seconds 0 > $O/bench_stress128_bf16x3.json 2> $O/bench_stress128_bf16x3.err &&
-timeout -k 10 300 python3 bench.py --osc 8192 --envs 1024 --coupling bf16x3 --steps 4 --warmup 2 --cpu-seconds 0 > $O/bench_stress1024_bf16x3.json 2> $O/bench_stress1024_bf16x3.err &&
+timeout -k 10 300 python3 bench.py --osc 8192 --envs 128 --coupling f32 --steps 10 --warmup 2 --cpu-seconds 0 > $O/bench_stress128_f32.json 2> $O/bench_stress128_f32.err &&
+timeout -k 10 300 python3 bench.py --osc 8192 --envs 1024 --coupling f32 --steps 4 --warmup 2 --cpu-seconds 0 > $O/bench_stress1024_f32.json 2> $O/bench_stress1024_f32.err &&
 bash tools/rocprof_run.sh ${T}_prof > $O/rocprof.log 2>&1 &&
 bash tools/pmc_pass.sh ${T}_pmc > $O/pmc.log 2>&1 &&
 timeout -k 10 300 python3 tools/phase_stamps.py > $O/stamps_step.json 2> $O/stamps_step.err
