@@ -230,3 +230,22 @@ def test_rhs_matches_reference_op_sequence_n8192(coupling):
         f = o.rhs(y, G8["rhs_n8192_w0"], G8["rhs_n8192_pulse"])
         np.testing.assert_allclose(f, f_ref, rtol=0, atol=RHS_ATOL, err_msg=coupling)
     o.close()
+
+
+def test_auto_is_bf16x3_at_n8192():
+    """AUTO resolves to BF16X3 above N = 1024 as well, in the Python mirror
+    (abi.coupling_of) and in kura.h's kura_coupling_of as compiled into the
+    oracle: the AUTO oracle's RHS is bit for bit the BF16X3 one, and differs
+    from the F32 one."""
+    alpha = ms.coupling_alpha(G8["rhs_n8192_coords"]).astype(np.float32)
+    p = kura.synthetic_params("env0", 8192)
+    y, w0, pulse = G8["rhs_n8192_y"][0], G8["rhs_n8192_w0"], G8["rhs_n8192_pulse"]
+    f = {}
+    for c in ("auto", "bf16x3", "f32"):
+        cfg = sim_mod.make_config(p, 1, reward_func="bbpow_action", coupling=c)
+        o = ko.Oracle(cfg, alpha)
+        f[c] = o.rhs(y, w0, pulse)
+        o.close()
+    assert kura.coupling_of(sim_mod.make_config(p, 1, reward_func="bbpow_action")) == "bf16x3"
+    np.testing.assert_array_equal(f["auto"], f["bf16x3"])
+    assert not np.array_equal(f["bf16x3"], f["f32"])
