@@ -69,9 +69,19 @@ def test_rocprof_summary_backs_the_bench_roofline():
     import json
     bench = importlib.import_module("bench")
     d = json.load(open(f"{ROOT}/profiles/latest_rocprof.json"))
-    k = d["kernels"][bench.kernel_name(1024, 0, "bf16x3")]       # the product arithmetic at N=1024
-    traffic, src, clock = bench.pmc_traffic(1024, 4096, 0, "bf16x3")
-    assert traffic == k["traffic_bytes_per_dispatch"] > 0
-    assert d["source"] in src and 1.3 < clock < 2.6
-    hip_ms = d["bench_under_trace"]["avg_kernel_ms_hip_events"]
-    assert k["min_ms"] <= hip_ms and abs(k["avg_ms"] - hip_ms) / hip_ms < 0.05
+    import glob
+    paths = sorted(glob.glob(f"{ROOT}/profiles/latest_rocprof*.json"))
+    assert f"{ROOT}/profiles/latest_rocprof.json" in paths
+    for path in paths:     # the headline and each N=8192 form: one summary per workload
+        d = json.load(open(path))
+        wl = d["bench_under_trace"]["config"]["workload"]
+        n = int(wl.split("N=")[1].split()[0])
+        part = d["bench_under_trace"]["config"].get("part_osc", 0)
+        kname = bench.kernel_name(n, part, "bf16x3")                 # the product arithmetic (AUTO)
+        k = d["kernels"][kname]
+        traffic, src, clock = bench.pmc_traffic(wl, kname)
+        assert traffic == k["traffic_bytes_per_dispatch"] > 0, path
+        assert d["source"] in src and os.path.basename(path) in src and 1.3 < clock < 2.6
+        hip_ms = d["bench_under_trace"]["avg_kernel_ms_hip_events"]
+        assert k["min_ms"] <= hip_ms * 1.001 and abs(k["avg_ms"] - hip_ms) / hip_ms < 0.05, path
+    assert bench.pmc_traffic("no such workload", kname) == (None, None, None)
