@@ -11,7 +11,7 @@ import ctypes
 import os
 from ctypes import POINTER, c_double, c_float, c_int, c_int32, c_int64, c_uint8, c_void_p
 
-KURA_ABI_VERSION = 1
+KURA_ABI_VERSION = 2   # include/kura.h (2: KuraConfig.coupling, AUTO = BF16X3)
 KURA_S_MAX = 32
 KURA_MAX_BINS = 32
 KURA_NSTATS = 8

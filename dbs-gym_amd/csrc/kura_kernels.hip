@@ -254,7 +254,8 @@ __device__ __forceinline__ T* uniform_ptr(T* ptr) {
 // three-way bf16 splits on v_mfma_f32_32x32x16_bf16, six part products per
 // 16-deep k-block in the order x1a1, x1a2, x2a1, x1a3, x2a2, x3a1 (the oracle
 // restates the MFMA's accumulation exactly: oracle_split_gemm_rows, pinned by
-// tests/test_mfma_bf16_model.py and tests/test_gpu_split_gemm.py).  alpha
+// tests/test_mfma_bf16_model.py and the bitwise GEMM tests of
+// tests/test_gpu_parity.py).  alpha
 // arrives pre-split (split_alpha, kura_capi.inc): per column tile jt, k-block
 // b and part p, lane l holds 8 bf16 at k = 16b + 8(i/4) + 2(i%4) + l/32 -- the
 // k order of the fp32 operand image, so the sin/cos rows are split from the

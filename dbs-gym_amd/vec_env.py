@@ -22,6 +22,7 @@ import numpy as np
 import torch
 
 from . import spectral
+from . import abi
 from .abi import KURA_S_MAX
 from .batch import EnvHost, build_batch, fill_driver_arrays, fill_driver_arrays_batch, log_temporal_events, reset_draws_batch
 from .abi import KuraSolverError
@@ -318,8 +319,19 @@ class KuraVectorEnv:
         lo, hi = self.cfg.dbs_lo, self.cfg.dbs_hi
         x, y = self.cfg.act_lo, self.cfg.act_hi
         self.u = lo + ((hi - lo) * (a.double() - x)) / (y - x)      # env.py:389-393 (for callers)
+        pre_metrics = None
+        if trunc is not None and self.episode_metrics:
+            # the truncated episodes ended with the failed call: their metrics
+            # come from the episode buffer as it stands before this launch (whose
+            # step for them is discarded) may append to it
+            m = torch.zeros(self.num_envs, dtype=torch.uint8)
+            m[trunc[0]] = 1
+            pre_metrics = (self.sim.episode_bbpow(m, self.psd_dt, self.beta_band).clone(),
+                           self.sim.episode_envelope_stats(m).clone())
         obs, rew, done = self.sim.step(a)
         self.steps += 1
+        if trunc is not None:
+            self.steps[trunc[0]] -= 1      # the discarded step is not part of the truncated episode
         # next_step mode: the envs that finished in the previous call are reset
         # in this one -- their step above is discarded (the reset below
         # overwrites its state and outputs)
@@ -376,9 +388,13 @@ class KuraVectorEnv:
                 mask = torch.zeros(self.num_envs, dtype=torch.uint8)
                 mask[idx] = 1
                 bb = self.sim.episode_bbpow(mask, self.psd_dt, self.beta_band)
-                infos["episode"]["bbpow"] = bb[torch.as_tensor(idx, device=self.device)].cpu().numpy()
                 # per_episode/envelope/{mean,std,cum} of the training callback (custom_callbacks.py:146-148)
                 ev = self.sim.episode_envelope_stats(mask)
+                if pre_metrics is not None:
+                    td = torch.as_tensor(trunc[0], device=self.device)
+                    bb, ev = bb.clone(), ev.clone()
+                    bb[td], ev[td] = pre_metrics[0][td], pre_metrics[1][td]
+                infos["episode"]["bbpow"] = bb[torch.as_tensor(idx, device=self.device)].cpu().numpy()
                 infos["episode"]["envelope"] = ev[torch.as_tensor(idx, device=self.device)].cpu().numpy()
             tb["metrics_s"] = time.perf_counter() - t0
         if nxt is not None:   # next_step mode: reset observation, reward 0, not done
@@ -634,12 +650,19 @@ class KuraVectorEnv:
     def state_dict(self):
         """Checkpointable env state (phases, times, counters, windows)."""
         st = self.sim.get_state()
+        # the arithmetic the trajectories were computed in: a run continues
+        # bit for bit only in the same one (kura.h KURA_COUPLING_*)
+        st["coupling"] = abi.coupling_of(self.sim.cfg)
         st["host_steps"] = self.steps.copy()
         st["rng"] = [h.rs.get_state() for h in self.hosts]
         st["reset_count"] = [h.reset_count for h in self.hosts]
         return st
 
     def load_state_dict(self, st):
+        have = abi.coupling_of(self.sim.cfg)
+        if st.get("coupling", have) != have:
+            raise ValueError(f"state_dict was saved with coupling={st['coupling']!r}; this env runs {have!r} "
+                             "(pass coupling= to KuraVectorEnv)")
         self.sim.set_state(st)
         self.steps[:] = st["host_steps"]
         for h, s, rc in zip(self.hosts, st["rng"], st["reset_count"]):

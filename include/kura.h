@@ -48,7 +48,11 @@
 extern "C" {
 #endif
 
-#define KURA_ABI_VERSION 1
+/* ABI history.  1: rounds 1-4.  2: KuraConfig.coupling takes the former
+ * reserved_i[0] slot (0 = AUTO, which resolves to BF16X3: a zero-filled
+ * version-1 config would silently change arithmetic, so kura_create rejects
+ * abi_version 1), kura_set_transient_capture, kura_selftest_coupling. */
+#define KURA_ABI_VERSION 2
 #define KURA_S_MAX 32   /* max LFP samples emitted by one step (ref: 17-19) */
 #define KURA_MAX_BINS 32
 

@@ -105,3 +105,22 @@ def test_metric_entry_points_reject_null_handle():
     assert lib.kura_episode_envelope_stats(None, None, None, None) == -1
     assert lib.kura_psd_bbpow(None, None, None, 16, 1, 5e-4, 12.5, 21.0, None, None) == -1
     assert lib.kura_episode_bbpow(None, None, 5e-4, 12.5, 21.0, None, None) == -1
+
+
+def test_version_1_config_is_rejected():
+    """the coupling field reuses version 1's reserved slot (0 = AUTO
+    = BF16X3), so a version-1 config is refused with KURA_E_INVALID before any
+    HIP call, naming the field to choose."""
+    if not os.path.exists(abi.LIB_PATH):
+        pytest.skip("libkura.so not built")
+    assert abi.KURA_ABI_VERSION == 2
+    lib = abi.load_library()
+    sim = importlib.import_module("dbs-gym_amd.sim")
+    kura = importlib.import_module("dbs-gym_amd")
+    cfg = sim.make_config(kura.reference_params("env0"), 4, reward_func="bbpow_action")
+    assert cfg.abi_version == 2
+    cfg.abi_version = 1
+    h = ctypes.c_void_p()
+    assert lib.kura_create(ctypes.byref(cfg), 0, ctypes.byref(h)) == -1   # KURA_E_INVALID
+    msg = lib.kura_last_error().decode()
+    assert "abi_version 1 != 2" in msg and "coupling" in msg

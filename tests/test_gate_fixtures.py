@@ -31,9 +31,9 @@ def test_record_prefix_is_the_oracle(scenario, steps, monkeypatch):
 def test_records_hold_the_gate():
     """Each record reaches step 1000 with a finite state, the env2 one through
     three autoresets (reset step counters back at 0 at steps 300/600/900)."""
-    for name in gs.SCENARIOS:
+    for name, (_, _, _, envs) in gs.SCENARIOS.items():
         R = np.load(os.path.join(GOLDEN, f"gate_{name}.npz"))
-        assert R["rewards"].shape == (gs.STEPS, gs.B)
+        assert R["rewards"].shape == (gs.STEPS, envs)
         assert np.all(np.isfinite(R["rewards"])) and np.all(np.isfinite(R["s1000_y"]))
         if name == "env2_r1_vec":
             assert R["s1000_t"].min() > 200.0 + 80.0   # the transient + 100 steps since the third reset
@@ -60,3 +60,18 @@ def test_stress_records_hold_three_steps():
         np.testing.assert_array_equal(R[f"s{ss.STEPS}_step"], ss.STEPS)
         assert np.all(R[f"s{ss.STEPS}_t"] > R["reset_t"])
         assert all(np.all(np.isfinite(R[f"s{k}_reward"])) for k in range(1, ss.STEPS + 1))
+
+
+@pytest.mark.parametrize("name", ["env0_r1", "env1_r2"])
+def test_b32_records_extend_the_b8_records(name):
+    """Env b draws the same inputs and actions at any batch size, and the
+    oracle steps every env on its own, so the first 8 envs of the B=32 record
+    (two full workgroups on the GPU) are the B=8 record: rewards of every step
+    and the checkpoint states."""
+    R8 = np.load(os.path.join(GOLDEN, f"gate_{name}.npz"))
+    R32 = np.load(os.path.join(GOLDEN, f"gate_{name}_b32.npz"))
+    np.testing.assert_array_equal(R32["rewards"][:, :8], R8["rewards"])
+    for tag in ("reset",) + tuple(f"s{c}" for c in gs.CHECK):
+        for k in gs.STATE_KEYS:
+            np.testing.assert_array_equal(R32[f"{tag}_{k}"][:8], R8[f"{tag}_{k}"], err_msg=f"{tag}_{k}")
+    np.testing.assert_array_equal(R32["final_ring"][:8], R8["final_ring"])

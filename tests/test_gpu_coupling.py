@@ -1,6 +1,6 @@
 """KuraConfig.coupling (kura.h KURA_COUPLING_*) on the GPU: the arithmetic is
 a run-time choice of the one libkura.so, AUTO resolves as the oracle resolves
-it (BF16X3 for N <= 1024, F32 for split env groups), each choice is a twin of
+it (BF16X3 at every N, split env groups included), each choice is a twin of
 the oracle in that arithmetic (tests/test_gpu_parity.py, tests/test_gpu_gates.py),
 and a choice the library does not implement is refused, not run wrong."""
 import importlib

@@ -340,6 +340,34 @@ def test_deferred_failure_next_step_mode_ends_the_episode_then_resets(torch_gpu)
     env.close()
 
 
+def test_next_step_truncation_excludes_the_discarded_step(torch_gpu):
+    """next_step mode with deferred checks, the failure of call k
+    ends the episode in call k+1, whose step for that env is discarded: the
+    episode length counts calls 1..k only, and the episode metrics are those
+    of the episode buffer as call k left it."""
+    kura = importlib.import_module("dbs-gym_amd")
+    venv = importlib.import_module("dbs-gym_amd.vec_env")
+    env = _short_env(venv, kura, 3, 50, autoreset_mode="next_step", episode_metrics=True)
+    env.reset()
+    a = np.zeros((3, 1), np.float32)
+    env.step(a)
+    env.step(a)
+    _poison(env, 1)
+    env.step(a)                                               # call k = 3 fails on the device
+    m = torch_gpu.zeros(3, dtype=torch_gpu.uint8)
+    m[1] = 1
+    want_bb = env.sim.episode_bbpow(m, env.psd_dt, env.beta_band)[1].item()
+    want_ev = env.sim.episode_envelope_stats(m)[1].cpu().numpy().copy()
+    obs, rew, term, trunc, info = env.step(a)                 # call k+1: ends the episode, its step discarded
+    assert list(info["failed_env_ids"]) == [1] and bool(trunc[1])
+    ids = list(info["terminal_env_ids"])
+    assert ids == [1]
+    assert int(info["episode"]["l"][0]) == 3                 # calls 1..3, not the discarded 4th
+    assert info["episode"]["bbpow"][0] == want_bb
+    np.testing.assert_array_equal(info["episode"]["envelope"][0], want_ev)
+    env.close()
+
+
 def test_deferred_failure_on_terminal_step_next_step_mode_resets_once(torch_gpu):
     """next_step mode, the failing step is the episode's last: the
     env is queued for its next_step reset; the deferred report must not reset

@@ -57,13 +57,15 @@ def _phase_gate(y, want):
     np.testing.assert_array_equal(y, want)
 
 
-@pytest.mark.parametrize("scenario", ["env0_r1", "env1_r2"])
+@pytest.mark.parametrize("scenario", ["env0_r1", "env1_r2", "env0_r1_b32", "env1_r2_b32"])
 def test_gate_1000_steps_product_arithmetic(torch_gpu, scenario):
+    """B=8 (half a workgroup) and B=32 (two full 16-env workgroups: every
+    lockstep slot active, per-env accept/reject masks interacting)."""
     torch = torch_gpu
     R = _record(scenario)
-    name, reward, act = gs.SCENARIOS[scenario]
+    name, reward, act, envs = gs.SCENARIOS[scenario]
     sim_mod = importlib.import_module("dbs-gym_amd.sim")
-    cfg, alpha, omega, g_s, g_r, th0, ct, st, _ = gs.env01_case(name, reward)
+    cfg, alpha, omega, g_s, g_r, th0, ct, st, _ = gs.env01_case(name, reward, envs=envs)
     assert kura.coupling_of(cfg) == "bf16x3"       # the product default at N=1024
     sim = sim_mod.KuraSim(cfg, 0)
     sim.set_coupling(alpha)
@@ -74,7 +76,7 @@ def test_gate_1000_steps_product_arithmetic(torch_gpu, scenario):
     _check_state(sim.get_state(), R, "reset")
     dig = gs.StepDigest()
     for k in range(gs.STEPS):
-        sim.step(torch.from_numpy(actions(act, gs.B, cfg.n_elec, k)))
+        sim.step(torch.from_numpy(actions(act, envs, cfg.n_elec, k)))
         rew = sim.reward.cpu().numpy()
         np.testing.assert_array_equal(rew, R["rewards"][k], err_msg=f"reward step {k}")
         dig.add(sim.obs.cpu().numpy(), rew, sim.done.cpu().numpy(), sim.nsamp.cpu().numpy(),

@@ -5,7 +5,7 @@ kernels are built as a bit-exact twin of oracle/kura_oracle.c (DESIGN.md
 "Numerics"), so every comparison here is exact equality, which implies the
 1e-5 tolerance (asserted explicitly in test_phase_gate_1000_steps).
 Both coupling arithmetics (kura.h KURA_COUPLING_*) are twins: the product
-default (AUTO = BF16X3 for N <= 1024) and F32; the oracle follows the
+default (AUTO = BF16X3 at every N) and F32; the oracle follows the
 config.  The 1000-step gates here run the F32 coupling against the live
 oracle; the product arithmetic's gates replay committed oracle records
 (tests/test_gpu_gates.py).

@@ -189,3 +189,29 @@ def test_next_step_autoreset_mode_matches_same_step(torch_gpu):
         else:
             np.testing.assert_array_equal(nxt[k][0], same[k][0])
             assert nxt[k][1] == same[k][1]
+
+
+def test_state_dict_round_trip_keeps_the_coupling(torch_gpu):
+    """a checkpoint records the arithmetic its trajectories were
+    computed in; it restores bit for bit into an env of the same coupling and
+    is refused by one of the other (the continuation would differ)."""
+    vec = importlib.import_module("dbs-gym_amd.vec_env")
+    p = kura.reference_params("env0", "eval", 1)
+    a = np.linspace(-1, 1, 3, dtype=np.float32).reshape(3, 1)
+    env = vec.KuraVectorEnv(copy.deepcopy(p), num_envs=3, reward_func="bbpow_action")
+    env.reset(seed=5)
+    env.step(a)
+    st = env.state_dict()
+    assert st["coupling"] == "bf16x3"                         # AUTO
+    _, r1, _, _, _ = env.step(a)
+    env2 = vec.KuraVectorEnv(copy.deepcopy(p), num_envs=3, reward_func="bbpow_action")
+    env2.reset(seed=9)
+    env2.load_state_dict(st)
+    _, r2, _, _, _ = env2.step(a)
+    np.testing.assert_array_equal(r1.cpu().numpy(), r2.cpu().numpy())
+    env3 = vec.KuraVectorEnv(copy.deepcopy(p), num_envs=3, reward_func="bbpow_action", coupling="f32")
+    env3.reset(seed=5)
+    with pytest.raises(ValueError, match="coupling"):
+        env3.load_state_dict(st)
+    for e in (env, env2, env3):
+        e.close()
