@@ -105,3 +105,22 @@ def test_spilled_mask_census_reads_compiler_listings():
                      "\ts_or_b64 exec, exec, s[22:23]"])
     r = chk.find_spilled_store_masks(chk.parse_asm(asm))
     assert [(n, v, k) for n, _i, v, k in r] == [("f", "v252", 1)]
+
+
+@pytest.mark.parametrize("name", ["libkura.so", "libkura_debug.so"])
+def test_spilled_mask_census_within_reviewed_baseline(name):
+    """the census is gated against its reviewed baseline
+    (tools/store_mask_baseline.json; sites mapped by tools/store_mask_sites.py,
+    executed by tests/test_gpu_store_sites.py): a kernel edit that adds a
+    store of this shape fails the build until it is reviewed."""
+    import json
+    lib = os.path.join(CSRC, name)
+    if not os.path.exists(lib):
+        pytest.skip(f"{name} not built")
+    base = json.load(open(chk.BASELINE))["stores_per_function"]
+    _n, _hz, sm = chk.check_library(lib)
+    assert chk.over_baseline(lib, sm, base) == []
+    # one more store in a known function, or a site in a new one, is over
+    extra = sm + [(sm[0][0], 0, "v250", 1), ("new_fn", 0, "v250", 1)]
+    over = chk.over_baseline(lib, extra, base)
+    assert [f for f, _k, _b in over] == sorted([sm[0][0], "new_fn"])

@@ -237,9 +237,33 @@ def check_library(lib: str):
     return nstores, find_hazards(funcs), find_spilled_store_masks(funcs)
 
 
+BASELINE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "store_mask_baseline.json")
+
+
+def census_key(sm):
+    """{function: stores under a spilled exec mask} of a census."""
+    out = {}
+    for name, _i, _v, k in sm:
+        out[name] = out.get(name, 0) + k
+    return out
+
+
+def over_baseline(lib, sm, baseline):
+    """Functions whose spilled-mask stores exceed the committed baseline
+    (tools/store_mask_baseline.json): a new site needs an explicit review --
+    map it (tools/store_mask_sites.py), name the GPU test that executes it,
+    then raise the baseline."""
+    base = baseline.get(os.path.basename(lib), {})
+    return sorted((f, k, base.get(f, 0)) for f, k in census_key(sm).items() if k > base.get(f, 0))
+
+
 def main(argv):
+    import json
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    gate = "--baseline" in argv
+    argv = [a for a in argv if a != "--baseline"]
     libs = argv or [os.path.join(root, "dbs-gym_amd", "csrc", n) for n in ("libkura.so", "libkura_debug.so")]
+    baseline = json.load(open(BASELINE))["stores_per_function"] if gate else {}
     bad = 0
     for lib in libs:
         if not os.path.exists(lib):
@@ -248,12 +272,17 @@ def main(argv):
             continue
         n, hz, sm = check_library(lib)
         print(f"{os.path.basename(lib)}: {n} wide VMEM stores, {len(hz)} store-data hazards, "
-              f"{len(sm)} stores under a spilled exec mask")
+              f"{len(sm)} sites / {sum(k for *_r, k in sm)} stores under a spilled exec mask")
         for name, a, m, o, b, bm, ws in hz[:20]:
             print(f"  {name}: {m} {o} @0x{a:x} <- {bm} @0x{b:x} after {ws} wait state(s)")
-        for name, i, v, k in sm[:20]:
+        for name, i, v, k in sm[:40]:
             print(f"  {name}: {k} store(s) under a mask read back from {v} (instruction {i})")
-        bad += bool(hz)   # the spilled-mask census is reported, not gated
+        bad += bool(hz)
+        if gate:   # the spilled-mask census may not grow past its reviewed baseline
+            over = over_baseline(lib, sm, baseline)
+            for f, k, b in over:
+                print(f"  OVER BASELINE: {f}: {k} stores under a spilled exec mask (baseline {b})")
+            bad += bool(over)
     return 1 if bad else 0
 
 
