@@ -564,6 +564,8 @@ def main(argv=None):
                       "frac_of_peak_at_effective_clock": (exec_tf / (peak_tf * clock_ghz / 2.4)
                                                           if clock_ghz else None),
                       "reset_ms": t_reset * 1e3, "reset_rhs_max": int(reset_stats[0]),
+                      **({"xl_launch": "plain" if os.environ.get("KURA_XL_LAUNCH") == "plain" else "cooperative"}
+                         if N > 1024 else {}),
                       "host_setup_s": t_setup},
         }
     if args.episode:

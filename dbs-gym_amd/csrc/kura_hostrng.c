@@ -112,6 +112,26 @@ void kh_seed(kh_mt* streams, const int64_t* rows, const uint32_t* seeds, int64_t
     for (int64_t i = 0; i < n; ++i) kh_init_genrand(&streams[rows[i]], seeds[i]);
 }
 
+// streams[row].randint(low, high) with size=None, 1 <= high - low <= 2^32:
+// numpy's legacy bounded integers (random_bounded_uint64_fill, masked
+// rejection on 32-bit draws; RandomState.choice(a) draws its index this way).
+int64_t kh_randint(kh_mt* streams, int64_t row, int64_t low, int64_t high) {
+    const uint64_t rng = (uint64_t)(high - 1 - low);
+    if (rng == 0) return low;
+    kh_mt* s = &streams[row];
+    if (rng == 0xFFFFFFFFull) return low + (int64_t)kh_next32(s);
+    uint64_t mask = rng;
+    mask |= mask >> 1;
+    mask |= mask >> 2;
+    mask |= mask >> 4;
+    mask |= mask >> 8;
+    mask |= mask >> 16;
+    uint32_t val;
+    while ((val = kh_next32(s) & (uint32_t)mask) > rng) {
+    }
+    return low + (int64_t)val;
+}
+
 // out[i, :m] <- streams[rows[i]].random_sample(m)
 void kh_random_sample(kh_mt* streams, const int64_t* rows, int64_t n, int64_t m, double* out) {
 #pragma omp parallel for schedule(static)

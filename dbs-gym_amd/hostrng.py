@@ -6,8 +6,8 @@ utils.py:819-823, :868, :927).  ``StreamBank`` holds the states of B such
 streams in one array and draws for many envs per call; ``Stream`` is one env's
 view with the RandomState methods the host code uses.  Every draw is bit for
 bit what ``numpy.random.RandomState(seed)`` returns for the same calls
-(tests/test_hostrng.py); methods it does not implement natively (``choice``,
-``randint``, ...) run on a scratch RandomState loaded with this stream's state
+(tests/test_hostrng.py); methods it does not implement natively (``shuffle``,
+``choice`` with a size or p, ...) run on a scratch RandomState loaded with this stream's state
 and store the advanced state back, so any RandomState call is available with
 the same results.
 """
@@ -35,6 +35,8 @@ def lib():
         P, I64, D = ctypes.c_void_p, ctypes.c_int64, ctypes.c_double
         L.kh_state_size.restype = ctypes.c_int
         L.kh_state_size.argtypes = []
+        L.kh_randint.restype = I64
+        L.kh_randint.argtypes = [P, I64, I64, I64]
         for name, args in (("kh_seed", [P, P, P, I64]),
                            ("kh_random_sample", [P, P, I64, I64, P]),
                            ("kh_uniform", [P, P, I64, P, P, I64, P]),
@@ -140,6 +142,10 @@ class StreamBank:
                                float(step_scale), _ptr(out), _ptr(tmp))
         return out
 
+    def randint(self, row: int, low: int, high: int) -> int:
+        """RandomState.randint(low, high) (size=None) on stream row."""
+        return int(lib().kh_randint(_ptr(self.state), int(row), int(low), int(high)))
+
     def randn(self, row: int, m: int) -> np.ndarray:
         out = np.empty(int(m))
         lib().kh_randn(_ptr(self.state), int(row), int(m), _ptr(out))
@@ -224,6 +230,25 @@ class Stream:
             return self._numpy("normal", loc, scale, size)
         n = _size_len(size)
         return self._shape(self.bank.normal([self.row], loc, scale, 1 if n is None else n)[0], size)
+
+    def randint(self, low, high=None, size=None, dtype=int):
+        if high is None:
+            low, high = 0, low
+        if size is None and dtype is int and np.ndim(low) == 0 and np.ndim(high) == 0 \
+                and 1 <= int(high) - int(low) <= 1 << 32:
+            return self.bank.randint(self.row, int(low), int(high))
+        return self._numpy("randint", low, high, size, dtype)
+
+    def choice(self, a, size=None, replace=True, p=None):
+        """RandomState.choice: one uniform index (size=None, replace, no p) is
+        randint(0, len(a)) -- native; anything else runs on the scratch state."""
+        if size is None and replace and p is None:
+            arr = np.asarray(a)
+            pop = int(arr) if arr.ndim == 0 else arr.shape[0]
+            if arr.ndim <= 1 and 1 <= pop <= 1 << 32:
+                idx = self.bank.randint(self.row, 0, pop)
+                return idx if arr.ndim == 0 else arr[idx]
+        return self._numpy("choice", a, size, replace, p)
 
     def randn(self, *shape):
         if not shape:

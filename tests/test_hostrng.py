@@ -149,3 +149,26 @@ def test_perturbations_match_generate_perturbations(m):
         want = ms.generate_perturbations(rs, init[i], M=20, step_scale=0.05)
         assert np.array_equal(got[i], want)
         assert _same_state(bank.get_state(i), rs.get_state())
+
+
+@pytest.mark.parametrize("seed", SEEDS)
+def test_native_choice_and_randint_match_randomstate(seed):
+    """choice(a) / randint(low, high) without size run natively
+    (kh_randint: numpy's legacy masked rejection on 32-bit draws), bit for bit
+    RandomState's values, types and states -- population sizes around powers
+    of two (rejection-heavy), 1 (no draw) and 2^32 (the unmasked case)."""
+    rs = np.random.RandomState(seed)
+    st = hr.StreamBank([seed]).stream(0)
+    calls = [("choice", ([-1, 0, 1],)), ("choice", ([-2, -1, 0, 1, 2],)), ("choice", ([0, 1],)), ("choice", (6,)),
+             ("choice", ([7],)), ("randint", (0, 1)), ("randint", (3, 20)), ("randint", (-5, 5)),
+             ("randint", (0, 2 ** 32)), ("randint", (0, 2 ** 31 + 1)), ("randint", (10,)), ("randint", (0, 65537)),
+             ("choice", (np.array([0.5, 1.5, 2.5]),))]
+    for k in range(60):
+        for name, a in calls:
+            x, y = getattr(rs, name)(*a), getattr(st, name)(*a)
+            assert x == y and type(x) is type(y), (k, name, a, x, y)
+            assert _same_state(rs.get_state(), st.get_state()), (k, name, a)
+    # the scratch-state route still serves the other forms
+    assert np.array_equal(rs.choice(5, 3), st.choice(5, 3))
+    assert np.array_equal(rs.choice([1, 2, 3], p=[0.2, 0.3, 0.5]), st.choice([1, 2, 3], p=[0.2, 0.3, 0.5]))
+    assert _same_state(rs.get_state(), st.get_state())
