@@ -66,6 +66,8 @@ def main(src, dst):
                 b = json.loads(f.read().strip().splitlines()[-1])
             out["bench_under_trace"] = {"value": b["value"], "avg_kernel_ms_hip_events": b["roofline"]["avg_kernel_ms"],
                                         "config": b["config"]}
+            if "xl_launch" in b.get("extra", {}):   # split groups: cooperative or plain (KURA_XL_LAUNCH) launch
+                out["bench_under_trace"]["xl_launch"] = b["extra"]["xl_launch"]
     with open(dst, "w") as f:
         json.dump(out, f, indent=1)
     print(json.dumps(out, indent=1))
