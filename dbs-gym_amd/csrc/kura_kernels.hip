@@ -1995,7 +1995,11 @@ __device__ KURA_SOLVE_ATTR void solve_wg(DevParamsK& __restrict__ pin, float* Xs
     STAMP(0);
     for (;;) {
         floatx16 acc[TPW];
+#ifdef KURA_EXP_NO_B1   // measurement-only upper bound (races: results invalid)
+        if (XL || s == 0 || s == 1) lds_barrier();
+#else
         lds_barrier();
+#endif
         STAMP(1);
         const float* xown = nullptr;
         if constexpr (XL) {
@@ -2038,7 +2042,11 @@ __device__ KURA_SOLVE_ATTR void solve_wg(DevParamsK& __restrict__ pin, float* Xs
 #endif
             coupling_epilogue<TPW, XL>(p, ws, Xs, xown, acc, s, pulse_on);
         STAMP(3);
+#ifdef KURA_EXP_NO_B2   // measurement-only upper bound (races: results invalid)
+        if (XL || s == 0 || s == 6) lds_barrier();
+#else
         lds_barrier();  // every wave is done reading the operand before it is rewritten
+#endif
         STAMP(4);
         ++nrhs;
         if (s > 0 && s < 6) {
