@@ -919,12 +919,21 @@ __device__ __forceinline__ void split8(const floatx4& a, const floatx4& b, float
     v[0] = a[0]; v[1] = a[1]; v[2] = a[2]; v[3] = a[3];
     v[4] = b[0]; v[5] = b[1]; v[6] = b[2]; v[7] = b[3];
 }
+// cache policy (aux) of the record loads / stores: 0 = default; measurement
+// builds set 2 (nt) to keep the record stream from evicting alpha in L2
+#ifndef KURA_REC_LD_AUX
+#define KURA_REC_LD_AUX 0
+#endif
+#ifndef KURA_REC_ST_AUX
+#define KURA_REC_ST_AUX 0
+#endif
 // lane's two env groups: half 0 -> envs 4h..4h+3, half 1 -> envs 8+4h..8+4h+3
 __device__ __forceinline__ void load8(const Slot& w, int slot, int t, float (&v)[8]) {
     w.check(slot, t);
-    const floatx4 a = __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(w.rs, w.voff, w.soff(slot, t), 0));
-    const floatx4 b =
-        __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(w.rs, w.voff + 1024, w.soff(slot, t), 0));
+    const floatx4 a = __builtin_bit_cast(
+        floatx4, __builtin_amdgcn_raw_buffer_load_b128(w.rs, w.voff, w.soff(slot, t), KURA_REC_LD_AUX));
+    const floatx4 b = __builtin_bit_cast(
+        floatx4, __builtin_amdgcn_raw_buffer_load_b128(w.rs, w.voff + 1024, w.soff(slot, t), KURA_REC_LD_AUX));
     split8(a, b, v);
 }
 // Store-data hazard ("The round-2 miscompiles,
@@ -947,7 +956,8 @@ __device__ __forceinline__ int opaque_vgpr(int v) {
     return v;
 }
 __device__ __forceinline__ void store_rec_b128(const floatx4& v, __amdgpu_buffer_rsrc_t rs, int voff, int soff) {
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u32, v), rs, opaque_vgpr(voff) + soff, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u32, v), rs, opaque_vgpr(voff) + soff, 0,
+                                           KURA_REC_ST_AUX);
 }
 __device__ __forceinline__ void store8(const Slot& w, int slot, int t, const float (&v)[8]) {
     // raw buffer stores through the same wave-uniform descriptor as the
