@@ -261,6 +261,36 @@ __device__ __forceinline__ T* uniform_ptr(T* ptr) {
 // k order of the fp32 operand image, so the sin/cos rows are split from the
 // same two float4 reads of the LDS operand.
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+#ifndef KURA_SPLIT_SCALAR
+// Pairwise: one v_cvt_pk_bf16_f32 (round to nearest even) per two values and
+// part, the bf16 pair widened back by a shift and a mask, the residual by one
+// v_pk_add_f32 -- 9 VALU per pair.  The same values as the scalar form (each
+// residual x - bf16(x) is exact in fp32).
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ unsigned pk_bf16(f32x2 x) { return __builtin_bit_cast(unsigned, __builtin_convertvector(x, bf16x2)); }
+__device__ __forceinline__ f32x2 unpk_bf16(unsigned u) {
+    return f32x2{__uint_as_float(u << 16), __uint_as_float(u & 0xffff0000u)};
+}
+__device__ __forceinline__ void split_bf16x3(floatx4 lo, floatx4 hi, bf16x8& h1, bf16x8& h2, bf16x8& h3) {
+    u32x4 a, b, c;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const f32x2 x = q < 2 ? f32x2{lo[2 * q], lo[2 * q + 1]} : f32x2{hi[2 * q - 4], hi[2 * q - 3]};
+        const unsigned ua = pk_bf16(x);
+        const f32x2 r1 = x - unpk_bf16(ua);
+        const unsigned ub = pk_bf16(r1);
+        const f32x2 r2 = r1 - unpk_bf16(ub);
+        a[q] = ua;
+        b[q] = ub;
+        c[q] = pk_bf16(r2);
+    }
+    h1 = __builtin_bit_cast(bf16x8, a);
+    h2 = __builtin_bit_cast(bf16x8, b);
+    h3 = __builtin_bit_cast(bf16x8, c);
+}
+#else
 __device__ __forceinline__ void split_bf16x3(floatx4 lo, floatx4 hi, bf16x8& h1, bf16x8& h2, bf16x8& h3) {
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
@@ -273,6 +303,7 @@ __device__ __forceinline__ void split_bf16x3(floatx4 lo, floatx4 hi, bf16x8& h1,
         h3[i] = (__bf16)(r1 - (float)b);
     }
 }
+#endif
 
 template <int TPW>
 __device__ __forceinline__ void coupling_gemm_bf16x3(const float* __restrict__ Xs, const float* __restrict__ alpha_sw,
