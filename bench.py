@@ -64,6 +64,8 @@ def parse(argv=None):
     ap.add_argument("--cpu-seconds", type=float, default=24.0,
                     help="bounded CPU-baseline budget in seconds (0 = skip), split over its legs")
     ap.add_argument("--seed", type=int, default=2024)
+    ap.add_argument("--reset-reps", type=int, default=1,
+                    help="time this many resets of the same state (extra.reset_ms_warm: the fastest after the first)")
     ap.add_argument("--random-k", action="store_true", help="per-env K ~ U(0.3, 0.8) (north_star 'random K')")
     # rehearsal of the N>1 path on a one-GPU box: every rank on cuda:0, gloo for the
     # barrier / max-over-ranks (RCCL cannot put two ranks on one device)
@@ -458,6 +460,12 @@ def main(argv=None):
     torch.cuda.synchronize()
     t_reset = time.perf_counter() - t0
     reset_stats = sim.stats()
+    t_reset_warm = []
+    for _ in range(args.reset_reps - 1):
+        t0 = time.perf_counter()
+        sim.reset(th)
+        torch.cuda.synchronize()
+        t_reset_warm.append(time.perf_counter() - t0)
 
     gen = torch.Generator(device=dev)
     gen.manual_seed(args.seed + rank)
@@ -563,7 +571,8 @@ def main(argv=None):
                       "effective_clock_ghz": clock_ghz,
                       "frac_of_peak_at_effective_clock": (exec_tf / (peak_tf * clock_ghz / 2.4)
                                                           if clock_ghz else None),
-                      "reset_ms": t_reset * 1e3, "reset_rhs_max": int(reset_stats[0]),
+                      "reset_ms": t_reset * 1e3,
+                      "reset_ms_warm": min(t_reset_warm) * 1e3 if t_reset_warm else None, "reset_rhs_max": int(reset_stats[0]),
                       **({"xl_launch": "plain" if os.environ.get("KURA_XL_LAUNCH") == "plain" else "cooperative"}
                          if N > 1024 else {}),
                       "host_setup_s": t_setup},

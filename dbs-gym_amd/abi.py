@@ -143,6 +143,8 @@ _SYMBOLS = {
     "kura_get_env_flags": (c_int, [c_void_p, c_void_p, c_void_p]),
     "kura_set_row_capture": (c_int, [c_void_p, c_void_p]),
     "kura_set_transient_capture": (c_int, [c_void_p, c_void_p]),
+    "kura_set_transient_rows": (c_int, [c_void_p, c_void_p]),
+    "kura_transient_len": (c_int, [c_void_p]),
     "kura_get_stamps": (c_int, [c_void_p, c_void_p]),
     "kura_selftest_math": (c_int, [c_void_p, c_void_p, c_void_p, c_int]),
     "kura_selftest_gemm": (c_int, [c_void_p, c_void_p, c_void_p, c_int]),

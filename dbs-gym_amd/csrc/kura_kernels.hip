@@ -66,6 +66,7 @@ struct DevParams {
     double bw_b[5], bw_a[5], bw_zi[4];
     float rtol, atol, kn, dt0;
     const float* alpha_sw;  // B-fragment swizzled coupling
+    const float* alpha_dd;  // BF16X3, N <= 1024: the deduplicated image too (the reset's GEMM, -DKURA_RESET_DEDUP)
     const float* omega;     // [B][N]
     const float* kn_env;    // [B] float32(K_b / N), per-env coupling gain
     const double* g_stim;   // [B][n_elec][N]
@@ -101,6 +102,9 @@ struct DevParams {
     float* rows;            // optional [B][KURA_S_MAX+1][N]: every saved row of a step (sol_state_, env.py:430,440)
     double* lfp_tr;         // optional [B][n_transient - 1]: the LFP of every transient row of a reset but the
                             // last (theta_record_transient, env.py:611); NULL: only the last W rows are evaluated
+    float* rows_tr;         // optional [B][n_transient][N]: every row of a reset's transient (sol_state after
+                            // reset(), env.py:610); NULL: not kept
+    int n_tr;               // rows per env of rows_tr (len(arange(0, transient_len, dt)))
     float* gemm_dump;       // KURA_DEBUG builds: [sweep][2][32][N] operand and coupling sums of workgroup 0
     int gemm_dump_n;        // ... sweeps to keep (kura_debug_gemm_dump)
 };
@@ -438,6 +442,79 @@ __device__ __forceinline__ void coupling_gemm_f32(const float* __restrict__ Xs, 
     }
 }
 
+// K1's BF16X3 GEMM reading alpha through the deduplicated image (the
+// split-group image: a map [NB][N/32] of int32 byte offsets, then the
+// distinct B fragments; 112 of 2048 at N = 1024, 336 KB -- always L2
+// resident).  Same fragments, same MFMAs in the same order as
+// coupling_gemm_bf16x3, so the sums are identical; the fragment offsets are
+// scalar loads one k-block ahead of the refill they serve.  Used by the
+// reset (-DKURA_RESET_DEDUP): over its ~457 sweeps the workgroups of an XCD
+// drift apart and the 6 MiB streamed image misses L2.
+template <int TPW>
+__device__ __forceinline__ void coupling_gemm_bf16x3_dd(const float* __restrict__ Xs, const float* __restrict__ alpha_dd,
+                                                        floatx16 (&acc)[TPW]) {
+    constexpr int N = TPW * 32 * NWAVES;
+    constexpr int NB = N / 16, NT = N / 32;
+    constexpr unsigned FRAG = 3 * 64 * 16;
+    int lane;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+#pragma unroll
+    for (int t = 0; t < TPW; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[t][r] = 0.0f;
+    const floatx4* xs4 = reinterpret_cast<const floatx4*>(Xs + (lane >> 5) * XS_HALF + (lane & 31) * 4);
+    const float* au = uniform_ptr(alpha_dd);
+    const unsigned IMG = (unsigned)NT * NB * 4u + (unsigned)NT * NB * FRAG;   // bound: every fragment distinct
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)au, 0, IMG, 0x00020000);
+    // the map through the constant address space: scalar loads (s_load_dword)
+    typedef const __attribute__((address_space(4))) int cint;
+    cint* mp = reinterpret_cast<cint*>(reinterpret_cast<uintptr_t>(au)) + wave * TPW;   // map row b: mp[b * NT + t]
+    auto off = [&](int t, int b) -> int { return mp[b * NT + t]; };
+    auto ld = [&](int o, int p) -> bf16x8 {
+        return __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rs, (p * 64 + lane) * 16, o, 0));
+    };
+    bf16x8 a1[2][TPW], a2[2][TPW], a3[2][TPW];
+    int om[TPW];   // offsets of block b+2 (the next refill)
+#pragma unroll
+    for (int d = 0; d < 2; ++d)
+#pragma unroll
+        for (int t = 0; t < TPW; ++t) {
+            const int o = off(t, d);
+            a1[d][t] = ld(o, 0);
+            a2[d][t] = ld(o, 1);
+            a3[d][t] = ld(o, 2);
+        }
+#pragma unroll
+    for (int t = 0; t < TPW; ++t) om[t] = off(t, 2 < NB ? 2 : NB - 1);
+    auto blk = [&](int b, int d) __attribute__((always_inline)) {
+        bf16x8 x1, x2, x3;
+        split_bf16x3(xs4[(2 * b) * (XS_BLOCK / 4)], xs4[(2 * b + 1) * (XS_BLOCK / 4)], x1, x2, x3);
+        const int bn3 = b + 3 < NB ? b + 3 : NB - 1;
+#pragma unroll
+        for (int t = 0; t < TPW; ++t) {
+            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x1, a1[d][t], acc[t], 0, 0, 0);
+            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x1, a2[d][t], acc[t], 0, 0, 0);
+            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x2, a1[d][t], acc[t], 0, 0, 0);
+            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x1, a3[d][t], acc[t], 0, 0, 0);
+            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x2, a2[d][t], acc[t], 0, 0, 0);
+            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x3, a1[d][t], acc[t], 0, 0, 0);
+            const int o = om[t];
+            a1[d][t] = ld(o, 0);
+            a2[d][t] = ld(o, 1);
+            a3[d][t] = ld(o, 2);
+            om[t] = off(t, bn3);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    static_assert(NB % 2 == 0, "two-block ring");
+#pragma unroll 1
+    for (int b = 0; b < NB; b += 2) {
+        blk(b, 0);
+        blk(b + 1, 1);
+    }
+}
+
 // The coupling GEMM of a handle's arithmetic (SP: KURA_COUPLING_BF16X3).
 template <int TPW, bool SP>
 __device__ __forceinline__ void coupling_gemm(const float* __restrict__ Xs, const float* __restrict__ alpha_sw,
@@ -447,6 +524,10 @@ __device__ __forceinline__ void coupling_gemm(const float* __restrict__ Xs, cons
     else
         coupling_gemm_f32<TPW>(Xs, alpha_sw, acc, dbg);
 }
+
+#ifndef KURA_RESET_DEDUP
+#define KURA_RESET_DEDUP 0
+#endif
 
 // Workgroup barrier that orders LDS only.  Inside a solve every workspace
 // record (R) is written and read back by the same lane (MFMA-layout
@@ -1062,6 +1143,57 @@ __device__ __forceinline__ void coupling_epilogue(DevParamsK& __restrict__ p, co
 // ys = y0 + chain_j(kA[S][j] * (h f_j)), j < S, zero coefficients skipped
 // (the oracle's order: fp32 products h*f_j, the first term a product, the
 // rest fmas, then y0 + the chain)
+// Packed FP32 pairs (v_pk_mul_f32 / v_pk_add_f32 / v_pk_fma_f32: two IEEE
+// operations per instruction): the same operations in the same order as the
+// scalar forms they pair (kura_detmath.h), so the results are identical.
+typedef float kf2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ kf2 kf2_fma(kf2 a, kf2 b, kf2 c) { return __builtin_elementwise_fma(a, b, c); }
+// kdm_fold_reduce + kdm_sincos_red of two elements
+__device__ __forceinline__ void sincos_fold2(kf2 y, kf2& sn, kf2& cs, int& slow) {
+    const kf2 k = __builtin_elementwise_trunc(y * KDM_INV_TWO_PI_F);
+    const kf2 n = __builtin_elementwise_rint(y * KDM_TWO_OVER_PI_F);
+    const int j0 = (int)n.x - 4 * (int)k.x, j1 = (int)n.y - 4 * (int)k.y;
+    const kf2 jf = {(float)j0, (float)j1};
+    kf2 r = kf2_fma(-n, kf2(KDM_PIO2_C1), y);
+    r = kf2_fma(-jf, kf2(KDM_PIO2_C2), r);
+    r = kf2_fma(-jf, kf2(KDM_PIO2_C3), r);
+    slow |= (int)!(fabsf(y.x) < 4194304.0f) | (int)!(fabsf(y.y) < 4194304.0f);
+    const kf2 z = r * r;
+    kf2 ps = kf2_fma(z, kf2(-1.9515295891e-4f), kf2(8.3321608736e-3f));
+    ps = kf2_fma(z, ps, kf2(-1.6666654611e-1f));
+    const kf2 sr = kf2_fma(r * z, ps, r);
+    kf2 pc = kf2_fma(z, kf2(2.443315711809948e-5f), kf2(-1.388731625493765e-3f));
+    pc = kf2_fma(z, pc, kf2(4.166664568298827e-2f));
+    const kf2 cr = kf2_fma(z * z, pc, kf2_fma(kf2(-0.5f), z, kf2(1.0f)));
+    const int q0 = j0 & 3, q1 = j1 & 3;
+    float s0 = (q0 & 1) ? cr.x : sr.x, c0 = (q0 & 1) ? sr.x : cr.x;
+    float s1 = (q1 & 1) ? cr.y : sr.y, c1 = (q1 & 1) ? sr.y : cr.y;
+    s0 = (q0 & 2) ? -s0 : s0;
+    s1 = (q1 & 2) ? -s1 : s1;
+    c0 = ((q0 + 1) & 2) ? -c0 : c0;
+    c1 = ((q1 + 1) & 2) ? -c1 : c1;
+    sn = kf2{s0, s1};
+    cs = kf2{c0, c1};
+}
+// stage_ys of the element pair (q, q+1)
+template <int S>
+__device__ __forceinline__ kf2 stage_ys2(const float (&y0)[8], const float (&h)[8], const float (&f)[6][8], int q) {
+    const kf2 yy = {y0[q], y0[q + 1]};
+    if constexpr (S == 0) {
+        return yy;
+    } else {
+        const kf2 hh = {h[q], h[q + 1]};
+        auto hf = [&](int j) __attribute__((always_inline)) { return hh * kf2{f[j][q], f[j][q + 1]}; };
+        kf2 acc = kf2(kA[S][0]) * hf(0);
+        if constexpr (S > 1 && kA[S][1] != 0.0f) acc = kf2_fma(kf2(kA[S][1]), hf(1), acc);
+        if constexpr (S > 2) acc = kf2_fma(kf2(kA[S][2]), hf(2), acc);
+        if constexpr (S > 3) acc = kf2_fma(kf2(kA[S][3]), hf(3), acc);
+        if constexpr (S > 4) acc = kf2_fma(kf2(kA[S][4]), hf(4), acc);
+        if constexpr (S > 5) acc = kf2_fma(kf2(kA[S][5]), hf(5), acc);
+        return yy + acc;
+    }
+}
+
 template <int S>
 __device__ __forceinline__ void stage_ys(const float (&y0)[8], const float (&h)[8], const float (&f)[6][8],
                                          float (&ys)[8]) {
@@ -1080,6 +1212,22 @@ __device__ __forceinline__ void stage_ys(const float (&y0)[8], const float (&h)[
         }
     }
 }
+
+template <int S>
+__device__ __forceinline__ void stage_ys_pk(const float (&y0)[8], const float (&h)[8], const float (&f)[6][8],
+                                            float (&ys)[8]) {
+#pragma unroll
+    for (int q = 0; q < 8; q += 2) {
+        const kf2 v = stage_ys2<S>(y0, h, f, q);
+        ys[q] = v.x;
+        ys[q + 1] = v.y;
+    }
+}
+#ifdef KURA_SI_PACKED
+#define STAGE_YS stage_ys_pk
+#else
+#define STAGE_YS stage_ys
+#endif
 
 template <int TPW>
 __device__ __forceinline__ void stage_input(const Slot& ws, float* Xs, int s STAMP_PARAMS) {
@@ -1121,13 +1269,13 @@ __device__ __forceinline__ void stage_input(const Slot& ws, float* Xs, int s STA
         // lgkmcnt(0) wait per term and element, which also drained the LDS
         // writes of the tile before)
         switch (s) {
-            case 0: stage_ys<0>(y0[b], h, f[b], ys); break;
-            case 1: stage_ys<1>(y0[b], h, f[b], ys); break;
-            case 2: stage_ys<2>(y0[b], h, f[b], ys); break;
-            case 3: stage_ys<3>(y0[b], h, f[b], ys); break;
-            case 4: stage_ys<4>(y0[b], h, f[b], ys); break;
-            case 5: stage_ys<5>(y0[b], h, f[b], ys); break;
-            default: stage_ys<6>(y0[b], h, f[b], ys); break;
+            case 0: STAGE_YS<0>(y0[b], h, f[b], ys); break;
+            case 1: STAGE_YS<1>(y0[b], h, f[b], ys); break;
+            case 2: STAGE_YS<2>(y0[b], h, f[b], ys); break;
+            case 3: STAGE_YS<3>(y0[b], h, f[b], ys); break;
+            case 4: STAGE_YS<4>(y0[b], h, f[b], ys); break;
+            case 5: STAGE_YS<5>(y0[b], h, f[b], ys); break;
+            default: STAGE_YS<6>(y0[b], h, f[b], ys); break;
         }
         // theta = fmod(ys, 2pi_f) folded into the sincos reduction
         // (kdm_sincos_fmod2pi, kura_detmath.h): branch-free for the tile
@@ -1149,6 +1297,17 @@ __device__ __forceinline__ void stage_input(const Slot& ws, float* Xs, int s STA
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         STAMP(18);
+#elif defined(KURA_SI_PACKED)
+#pragma unroll
+        for (int q = 0; q < 8; q += 2) {
+            kf2 sn, cs;
+            sincos_fold2(kf2{ys[q], ys[q + 1]}, sn, cs, slow);
+            const int e0 = mfma_env(q, lane), e1 = mfma_env(q + 1, lane);
+            Xs[xs_idx(e0, i)] = sn.x;
+            Xs[xs_idx(16 + e0, i)] = cs.x;
+            Xs[xs_idx(e1, i)] = sn.y;
+            Xs[xs_idx(16 + e1, i)] = cs.y;
+        }
 #else
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
@@ -1322,16 +1481,29 @@ __device__ __forceinline__ void group_sum(DevParamsK& p, Part& pt, float (&vf)[N
     const size_t base = ((size_t)grp * 2 + (__builtin_amdgcn_readfirstlane(pt.ep) & 1)) * npart * (RC * E_WG);
     float* xr = p.xred + base;
     double* xd = p.xredd + base;
-    if (tid < E_WG)
-        for (int k = 0; k < nk; ++k) {  // write-through (sc1) stores
-            __hip_atomic_store((gu32*)(xr + (part * RC + k) * E_WG + tid), __float_as_uint(vf[k]),
-                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (with_d)
-                __hip_atomic_store((__attribute__((address_space(1))) unsigned long long*)(xd + (part * RC + k) *
-                                                                                              E_WG + tid),
-                                   (unsigned long long)__double_as_longlong(vd[k]), __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
+    // write-through (sc1) stores of this part's partials by all 64 lanes of
+    // wave 0 (a scalar branch): lanes >= E_WG get an offset past the
+    // descriptor's range, which the hardware drops -- no exec-masked store
+    // (hazards)
+    if (__builtin_amdgcn_readfirstlane(tid >> 6) == 0) {
+        constexpr int kSc1 = 16;          // cache policy: sc1 (write-through to memory)
+        constexpr int kDrop = 0x7ffffff0;
+        const bool wd = __builtin_amdgcn_readfirstlane((int)with_d) != 0;
+        const __amdgpu_buffer_rsrc_t rf =
+            __builtin_amdgcn_make_buffer_rsrc((void*)uniform_ptr(xr), 0, npart * RC * E_WG * 4, 0x00020000);
+        const __amdgpu_buffer_rsrc_t rd =
+            __builtin_amdgcn_make_buffer_rsrc((void*)uniform_ptr(xd), 0, npart * RC * E_WG * 8, 0x00020000);
+        for (int k = 0; k < nk; ++k) {
+            const int o = (part * RC + k) * E_WG + tid;
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(vf[k]), rf, tid < E_WG ? o * 4 : kDrop, 0, kSc1);
+            if (wd) {
+                const uint64_t u = (uint64_t)__double_as_longlong(vd[k]);
+                typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
+                __builtin_amdgcn_raw_buffer_store_b64(u32x2_t{(unsigned)u, (unsigned)(u >> 32)}, rd,
+                                                      tid < E_WG ? o * 8 : kDrop, 0, kSc1);
+            }
         }
+    }
     group_barrier(p, pt);
     if (tid < E_WG)
         for (int k = 0; k < nk; ++k) {
@@ -1489,9 +1661,34 @@ __device__ __forceinline__ void save_rounds_setup(const CtlE& c, int e, int r0) 
     }
 }
 
-template <int TPW, bool XL, int RCX>
-__device__ __forceinline__ void save_pass(DevParamsK& __restrict__ p, const Slot& ws, int env_base, bool to_ring, Part& pt,
+// Two save rounds at once on packed FP32 (v_pk_mul_f32 / v_pk_add_f32 /
+// v_pk_fma_f32 do two IEEE operations per instruction at the non-packed
+// instruction rate): kdm_cosf's cosine of both components, the same
+// operations in the same order as kdm_sincosf's c output (kura_detmath.h);
+// only the quadrant select stays per component.
+__device__ __forceinline__ kf2 kdm_cosf2(kf2 x) {
+    const kf2 j = __builtin_elementwise_rint(x * KDM_TWO_OVER_PI_F);
+    kf2 r = kf2_fma(-j, kf2(KDM_PIO2_C1), x);
+    r = kf2_fma(-j, kf2(KDM_PIO2_C2), r);
+    r = kf2_fma(-j, kf2(KDM_PIO2_C3), r);
+    const int q0 = ((int)j.x) & 3, q1 = ((int)j.y) & 3;
+    const kf2 z = r * r;
+    kf2 ps = kf2_fma(z, kf2(-1.9515295891e-4f), kf2(8.3321608736e-3f));
+    ps = kf2_fma(z, ps, kf2(-1.6666654611e-1f));
+    const kf2 sr = kf2_fma(r * z, ps, r);
+    kf2 pc = kf2_fma(z, kf2(2.443315711809948e-5f), kf2(-1.388731625493765e-3f));
+    pc = kf2_fma(z, pc, kf2(4.166664568298827e-2f));
+    const kf2 cr = kf2_fma(z * z, pc, kf2_fma(kf2(-0.5f), z, kf2(1.0f)));
+    float c0 = (q0 & 1) ? sr.x : cr.x, c1 = (q1 & 1) ? sr.y : cr.y;
+    c0 = ((q0 + 1) & 2) ? -c0 : c0;
+    c1 = ((q1 + 1) & 2) ? -c1 : c1;
+    return kf2{c0, c1};
+}
+
+template <int TPW, bool XL, int RCX, bool RS>
+__device__ __forceinline__ void save_pass(DevParamsK& __restrict__ p, const Slot& ws, int env_base, Part& pt,
                                           const float (&h)[8], int r0, int nrounds, bool gauss STAMP_PARAMS) {
+    constexpr bool to_ring = RS;   // a reset's transient (ring, rows_tr) or a step's solve (samples, rows)
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, tid = threadIdx.x;
     const int NG = XL ? __builtin_amdgcn_readfirstlane(pt.ng) : TPW * 256;
     const int col0 = XL ? __builtin_amdgcn_readfirstlane(pt.col0) : 0;
@@ -1552,7 +1749,14 @@ __device__ __forceinline__ void save_pass(DevParamsK& __restrict__ p, const Slot
     // unless the step's rows are captured (kura_set_row_capture)
     const int flor = fl[0] | fl[1] | fl[2] | fl[3] | fl[4] | fl[5] | fl[6] | fl[7];
     constexpr int kSave = (int)(01111111111u & ((1u << (3 * RCX)) - 1u));
-    const bool capture = p.rows != nullptr && !to_ring;
+    // captured rows: a step's into rows ([B][KURA_S_MAX+1][N], row = LFP
+    // position), a reset's into rows_tr ([B][n_tr][N], row = save index)
+    constexpr bool reset_rows = RS;
+    // (p is read through vector loads in the called solver: the capture switch
+    // and the descriptor fields are made wave-uniform, else the capture branch
+    // is divergent and its stores become exec-masked waterfall loops)
+    const bool capture = __builtin_amdgcn_readfirstlane((int)(reset_rows ? p.rows_tr != nullptr : p.rows != nullptr)) != 0;
+    const int crow = __builtin_amdgcn_readfirstlane(reset_rows ? p.n_tr : KURA_S_MAX + 1);   // captured rows per env
     const bool eval_rows = __any(flor & (capture ? kSave : kEval));  // rows to evaluate in any round
     int fin = 0;  // wave-uniform: rounds holding some env's final row (bit k)
 #pragma unroll
@@ -1563,19 +1767,23 @@ __device__ __forceinline__ void save_pass(DevParamsK& __restrict__ p, const Slot
     // hardware drops.  (Per-element exec-masked flat stores here lost almost
     // every final-state store of the split kernel with parts of 512 in some
     // builds -- the sums of the same pass were right -- DESIGN.md section 5.)
-    const int nvalid = Bn - env_base < E_WG ? Bn - env_base : E_WG;
+    // (env_base reaches this called solver in a VGPR: made wave-uniform, else
+    // the descriptors below are divergent and every store through them becomes
+    // a waterfall loop under an exec mask)
+    const int nvalid = __builtin_amdgcn_readfirstlane(Bn - env_base < E_WG ? Bn - env_base : E_WG);
     const __amdgpu_buffer_rsrc_t ys = __builtin_amdgcn_make_buffer_rsrc(
         (void*)uniform_ptr(p.y + (size_t)env_base * NG), 0, nvalid * NG * 4, 0x00020000);
+    float* const rows = reset_rows ? p.rows_tr : p.rows;
     const __amdgpu_buffer_rsrc_t rws = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)uniform_ptr(p.rows ? p.rows + (size_t)env_base * (KURA_S_MAX + 1) * NG : p.y), 0,
-        p.rows ? nvalid * (KURA_S_MAX + 1) * NG * 4 : 0, 0x00020000);
+        (void*)uniform_ptr(capture ? rows + (size_t)env_base * crow * NG : p.y), 0,
+        __builtin_amdgcn_readfirstlane(capture ? nvalid * crow * NG * 4 : 0), 0x00020000);
     constexpr int kDrop = 0x7ffffff0;   // past every range: the store is dropped
-    int rbase[8];  // captured row index of round 0 of this pass: sol_state_ row si - lfp_from + pos0
+    int rbase[8];  // captured row index of round 0 of this pass: sol_state_ row si - lfp_from + pos0 (step), si (reset)
     if (capture) {
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
             const CtlE& c = s_ctl[mfma_env(q, lane)];
-            rbase[q] = c.sv_si + r0 - c.lfp_from + c.pos0;
+            rbase[q] = reset_rows ? c.sv_si + r0 : c.sv_si + r0 - c.lfp_from + c.pos0;
         }
     }
     // (2) dense output + LFP partials: every (round, env) of a tile is
@@ -1659,7 +1867,7 @@ __device__ __forceinline__ void save_pass(DevParamsK& __restrict__ p, const Slot
 #pragma unroll
                         for (int qq = 0; qq < 4; ++qq) {
                             const int q = 4 * hh + qq;
-                            const int off = ((mfma_env(q, lane) * (KURA_S_MAX + 1) + rbase[q] + k) * NG + col0 + i) * 4;
+                            const int off = ((mfma_env(q, lane) * crow + rbase[q] + k) * NG + col0 + i) * 4;
                             __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[qq]), rws,
                                                                   ((fl[q] >> (3 * k)) & 1) ? off : kDrop, 0, 0);
                         }
@@ -1673,8 +1881,79 @@ __device__ __forceinline__ void save_pass(DevParamsK& __restrict__ p, const Slot
             }
         }
     }
+#ifdef KURA_SAVE_PACKED
+    // A/B form (measured and dropped): naive LFP rounds k, k+1 of a (tile,
+    // env) evaluated as one packed pair (kdm_cosf2).  A round past nk has
+    // flags 0 (save_rounds_setup), so its half of a pair adds +0 to its
+    // partial and stores nothing; a partial is never -0 (it starts at +0), so
+    // p + 0 == p and the sums are those of the scalar loop below, bit for bit
+    // (GPU suite green on it).  The pairs double the solver's scratch (436 ->
+    // 856 B per lane for <4, false, bf16x3>): same box, env0 step 3.02 ->
+    // 3.21-3.39 ms and reset 55 -> 83 ms (profiles/r06_save_packed_ab.txt).
+    constexpr bool kPk = !XL && (RCX % 2 == 0);
+#else
+    constexpr bool kPk = false;
+#endif
 #pragma unroll 1
-    for (int t = 0; t < (!XL && eval_rows ? TPW : 0); ++t) {
+    for (int t = 0; t < (kPk && !gauss && eval_rows ? TPW : 0); ++t) {
+        const int i = 32 * (wave * TPW + t) + (lane & 31);
+        float ca[8], cb[8], cc[8], f0[8], y0[8];
+        load8(ws, SL_CA, t, ca);
+        load8(ws, SL_CB, t, cb);
+        load8(ws, SL_CC, t, cc);
+        load8(ws, SL_F0, t, f0);
+        load8(ws, SL_Y0, t, y0);
+#ifdef KURA_STAMPS
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // attribute the record-load wait (diagnostic build)
+        STAMP(12);
+#endif
+        float k0[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) k0[q] = h[q] * f0[q];
+#pragma unroll
+        for (int k = 0; k < RCX; k += 2) {
+            if (k >= nk) break;  // wave-uniform: past every env's last save of this step
+            float v[2][8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                const kf2 x = {th[k][q], th[k + 1][q]};
+                kf2 w = kf2(ca[q]) * x + kf2(cb[q]);
+                w = w * x + kf2(cc[q]);
+                w = w * x + kf2(k0[q]);
+                w = w * x + kf2(y0[q]);
+                v[0][q] = w.x;
+                v[1][q] = w.y;
+                const kf2 cr = kdm_cosf2(w);
+                const int f = fl[q] >> (3 * k);
+                const kf2 add = {(f & 2) ? cr.x : 0.0f, (f & 020) ? cr.y : 0.0f};
+                const kf2 s = kf2{pn[k][q], pn[k + 1][q]} + add;
+                pn[k][q] = s.x;
+                pn[k + 1][q] = s.y;
+            }
+#pragma unroll
+            for (int kk = 0; kk < 2; ++kk) {
+                if ((fin >> (k + kk)) & 1) {  // the solve's last row: the new state
+#pragma unroll
+                    for (int q = 0; q < 8; ++q) {
+                        const int off = (mfma_env(q, lane) * NG + col0 + i) * 4;
+                        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[kk][q]), ys,
+                                                              ((fl[q] >> (3 * (k + kk))) & 4) ? off : kDrop, 0, 0);
+                    }
+                }
+                if (capture) {
+#pragma unroll
+                    for (int q = 0; q < 8; ++q) {
+                        const int off = ((mfma_env(q, lane) * crow + rbase[q] + k + kk) * NG + col0 + i) * 4;
+                        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[kk][q]), rws,
+                                                              ((fl[q] >> (3 * (k + kk))) & 1) ? off : kDrop, 0, 0);
+                    }
+                }
+            }
+        }
+        STAMP(13);
+    }
+#pragma unroll 1
+    for (int t = 0; t < (!XL && !(kPk && !gauss) && eval_rows ? TPW : 0); ++t) {
         const int i = 32 * (wave * TPW + t) + (lane & 31);
         float ca[8], cb[8], cc[8], f0[8], y0[8];
         double G[8];
@@ -1733,7 +2012,7 @@ __device__ __forceinline__ void save_pass(DevParamsK& __restrict__ p, const Slot
             if (capture) {
 #pragma unroll
                 for (int q = 0; q < 8; ++q) {
-                    const int off = ((mfma_env(q, lane) * (KURA_S_MAX + 1) + rbase[q] + k) * NG + col0 + i) * 4;
+                    const int off = ((mfma_env(q, lane) * crow + rbase[q] + k) * NG + col0 + i) * 4;
                     __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[q]), rws,
                                                           ((fl[q] >> (3 * k)) & 1) ? off : kDrop, 0, 0);
                 }
@@ -1820,8 +2099,8 @@ __device__ __forceinline__ void save_pass(DevParamsK& __restrict__ p, const Slot
 }
 
 // Returns whether any env of the workgroup goes on integrating (uniform).
-template <int TPW, bool XL>
-__device__ __forceinline__ int post_step(DevParamsK& __restrict__ p, Slot& ws, int env_base, bool to_ring, Part& pt
+template <int TPW, bool XL, bool RS>
+__device__ __forceinline__ int post_step(DevParamsK& __restrict__ p, Slot& ws, int env_base, Part& pt
                                          STAMP_PARAMS) {
     const int lane = threadIdx.x & 63, tid = threadIdx.x;
     const int NG = XL ? __builtin_amdgcn_readfirstlane(pt.ng) : TPW * 256;   // oscillators per env
@@ -1940,11 +2219,11 @@ __device__ __forceinline__ int post_step(DevParamsK& __restrict__ p, Slot& ws, i
     if (XL || gauss) {
 #pragma unroll 1
         for (int r0 = 0; r0 < nrounds; r0 += RC)
-            save_pass<TPW, XL, RC>(p, ws, env_base, to_ring, pt, h, r0, nrounds, gauss STAMP_ARGS);
+            save_pass<TPW, XL, RC, RS>(p, ws, env_base, pt, h, r0, nrounds, gauss STAMP_ARGS);
     } else {
 #pragma unroll 1
         for (int r0 = 0; r0 < nrounds; r0 += RC_N)
-            save_pass<TPW, XL, RC_N>(p, ws, env_base, to_ring, pt, h, r0, nrounds, false STAMP_ARGS);
+            save_pass<TPW, XL, RC_N, RS>(p, ws, env_base, pt, h, r0, nrounds, false STAMP_ARGS);
     }
     STAMP(8);
     // (4) accepted envs: y0 <- y1, f0 <- f6 (FSAL).  Envs that are not
@@ -1990,8 +2269,8 @@ __device__ __forceinline__ int post_step(DevParamsK& __restrict__ p, Slot& ws, i
 #else
 #define KURA_SOLVE_ATTR __noinline__
 #endif
-template <int TPW, bool XL, bool SP>
-__device__ KURA_SOLVE_ATTR void solve_wg(DevParamsK& __restrict__ pin, float* Xs, int env_base, bool to_ring, bool pulse_on,
+template <int TPW, bool XL, bool SP, bool RS>
+__device__ KURA_SOLVE_ATTR void solve_wg(DevParamsK& __restrict__ pin, float* Xs, int env_base, bool pulse_on,
                          long long* rhs_count, Part& pt) {
     // (the kernarg segment through the VGPR-passed pointer: vector loads.
     // Made wave-uniform -- scalar loads, which share lgkmcnt with the LDS
@@ -2073,7 +2352,12 @@ __device__ KURA_SOLVE_ATTR void solve_wg(DevParamsK& __restrict__ pin, float* Xs
                           (lane & 31)] = acc[t][q];
             }
 #else
-            coupling_gemm<TPW, SP>(Xs, p.alpha_sw, acc);
+#if KURA_RESET_DEDUP
+            if constexpr (SP && RS)
+                coupling_gemm_bf16x3_dd<TPW>(Xs, p.alpha_dd, acc);
+            else
+#endif
+                coupling_gemm<TPW, SP>(Xs, p.alpha_sw, acc);
 #endif
         }
         STAMP(2);
@@ -2098,7 +2382,7 @@ __device__ KURA_SOLVE_ATTR void solve_wg(DevParamsK& __restrict__ pin, float* Xs
         }
         int any;
         if (s == 6) {
-            any = post_step<TPW, XL>(p, ws, env_base, to_ring, pt STAMP_ARGS);   // advances time, sets h
+            any = post_step<TPW, XL, RS>(p, ws, env_base, pt STAMP_ARGS);   // advances time, sets h
             STAMP(10);
         } else {  // the solve's initial sweep: the first attempt's step size
             if (tid < E_WG && s_ctl[tid].active) s_ctl[tid].h = s_ctl[tid].tnext - s_ctl[tid].tprev;
@@ -2445,7 +2729,7 @@ __device__ __forceinline__ void step_pair(DevParamsK& p, Part& pt, float* Xs, co
             }
             __syncthreads();
         }
-        solve_wg<TPW, XL, SP>(p, Xs, env_base, false, ph == 0, &rhs, pt);
+        solve_wg<TPW, XL, SP, false>(p, Xs, env_base, ph == 0, &rhs, pt);
     }
     STAMP_DECL  // diagnostic build: the tail's phases in slots 20-22
     __syncthreads();
@@ -2621,7 +2905,7 @@ __device__ __forceinline__ void reset_pair(DevParamsK& p, Part& pt, float* Xs, c
     }
     __syncthreads();
     long long rhs = 0;
-    solve_wg<TPW, XL, SP>(p, Xs, env_base, true, false, &rhs, pt);
+    solve_wg<TPW, XL, SP, true>(p, Xs, env_base, false, &rhs, pt);
     __syncthreads();  // ring rows written by thread e are read by every lane below
 #pragma unroll 1
     for (int ee = 0; ee < ((!XL || pt.part == 0) ? ENVS_PER_WAVE : 0); ++ee) {

@@ -217,6 +217,22 @@ class KuraSim:
             check(self.lib, self.lib.kura_set_transient_capture(self._h, None), "kura_set_transient_capture")
             self.lfp_transient = None
 
+    def capture_transient_rows(self, on: bool = True) -> None:
+        """Keep the transient's rows of every reset in ``self.rows_transient``
+        (B, T, N) float32 -- the reference's sol_state after reset()
+        (env.py:610), row T-1 being the new state; T*N*4 bytes per env (16 MB
+        at N=1024), so meant for a few envs (kura_set_transient_rows)."""
+        if on:
+            T = self.lib.kura_transient_len(self._h)
+            if T <= 0:
+                check(self.lib, T if T < 0 else -1, "kura_transient_len")
+            self.rows_transient = torch.zeros((self.B, T, self.N), dtype=torch.float32, device=self.device)
+            check(self.lib, self.lib.kura_set_transient_rows(self._h, ptr(self.rows_transient)),
+                  "kura_set_transient_rows")
+        else:
+            check(self.lib, self.lib.kura_set_transient_rows(self._h, None), "kura_set_transient_rows")
+            self.rows_transient = None
+
     def failed_envs(self, mask: torch.Tensor | None = None):
         """(env indices, KURA_F_* bits) of the envs whose last launch failed (synchronises)."""
         f = self.flags.cpu().numpy()

@@ -680,8 +680,9 @@ class KuraVectorEnv:
                                   "kura_step (last call before close)")
 
 
-_SOL_STATE_AFTER_RESET = ("sol_state after reset() would be the transient's 4000 rows (env.py:610), which are not "
-                          "kept; step() first, or read the state (its last row) with get_state()['y']")
+_SOL_STATE_AFTER_RESET = ("sol_state after reset() is the transient's rows (env.py:610), kept only on request: "
+                          "call venv.sim.capture_transient_rows(True) before reset() (SpatialKuramoto does); "
+                          "or read the state (its last row) with get_state()['y']")
 
 # reference attributes the GPU path does not keep (no caller in the reference
 # reads them: aDBS_RL/, the notebooks); asking for them raises with the reason
@@ -707,6 +708,7 @@ class SpatialKuramoto:
                                 autoreset=False, failure_check="eager")
         self._v.sim.capture_rows(True)          # sol_state_: every row of the step (env.py:430,440)
         self._v.sim.capture_transient(True)     # theta_record_transient (env.py:611)
+        self._v.sim.capture_transient_rows(True)  # sol_state after reset() (env.py:610)
         self.action_space = self._v.single_action_space
         self.observation_space = self._v.single_observation_space
         self.current_step = 0
@@ -777,13 +779,16 @@ class SpatialKuramoto:
 
     @property
     def sol_state(self):
-        """The last solve's rows (env.py:429,439): after step(), the stim-OFF
-        solve's ys_II (sol_state_ from the duplicated I/II boundary row on).
-        After reset() the reference holds the transient's 4000 rows, which
-        the library does not keep (only its last row, the state): raises
-        AttributeError until the first step."""
+        """The last solve's rows (env.py:429,439, :610): after step(), the
+        stim-OFF solve's ys_II (sol_state_ from the duplicated I/II boundary
+        row on); after reset(), the transient's rows (T, N), T =
+        len(arange(0, transient_state_len, verbose_dt)), the last being the
+        state (kura_set_transient_rows)."""
         if getattr(self, "_n_on", None) is None:
-            raise AttributeError(_SOL_STATE_AFTER_RESET)
+            rt = getattr(self._v.sim, "rows_transient", None)
+            if rt is None:
+                raise AttributeError(_SOL_STATE_AFTER_RESET)
+            return rt[0].cpu().numpy()
         return self.sol_state_[self._n_on:]
 
     @property

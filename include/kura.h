@@ -282,6 +282,17 @@ int kura_set_row_capture(KuraHandle* h, float* rows_dev);
  * reset; off by default. */
 int kura_set_transient_capture(KuraHandle* h, double* lfp_dev);
 
+/* optional record of a reset's transient rows (env.py:610, sol_state =
+ * kuramoto.forward(t_eval_transient, init_state), read after reset()):
+ * rows_dev (device, B*T*N float32, T = kura_transient_len(h) =
+ * len(np.arange(0, transient_state_len, verbose_dt)), or NULL to stop)
+ * receives, for each env a kura_reset resets, every saved row of the
+ * transient, row T-1 being the new state.  Every row is then evaluated (as
+ * with kura_set_transient_capture) plus one store per value; off by
+ * default.  T*N*4 bytes per env: 16 MB at N=1024 -- meant for a few envs. */
+int kura_set_transient_rows(KuraHandle* h, float* rows_dev);
+int kura_transient_len(KuraHandle* h);   /* T above (> 0), or a negative KURA_E_* */
+
 /* per-env KURA_F_* bits of the last kura_step / kura_reset (0 = ok), copied
  * into the caller's device buffer out_dev (B int32) on the given stream:
  * read them with the step's outputs (no extra synchronisation). */

@@ -1,5 +1,6 @@
 """Boundary details callers read: sol_state_ keeps every
-row of the step, get_attr('u') is the reference's rescale_action bit for bit."""
+row of the step, sol_state after reset() the transient's rows (VERDICT r05
+missing #4), get_attr('u') is the reference's rescale_action bit for bit."""
 import importlib
 
 import numpy as np
@@ -56,11 +57,27 @@ def test_single_env_sol_state_rows():
     assert th0.dtype == np.float64 and th0.shape == (env._v.N,)
     env.reset()
     assert not np.array_equal(th0, env.init_state)
-    with pytest.raises(AttributeError, match="transient"):
-        env.sol_state
+    # sol_state after reset() (env.py:610): the transient's rows, the oracle's
+    # solve over arange(0, transient_state_len, verbose_dt) from init_state, bit
+    # for bit; the last row is the state
+    sol = env.sol_state
+    ts = np.arange(0.0, p["transient_state_len"], p["verbose_dt"])
+    assert sol.shape == (len(ts), env._v.N) and sol.dtype == np.float32
+    rows_o, _st = o.solve_rows(env._v._omega[0], None, ts, env.init_state.astype(np.float32))
+    np.testing.assert_array_equal(sol, rows_o)
+    np.testing.assert_array_equal(sol[-1], env._v.sim.get_state()["y"][0])
     # theta_record_transient (env.py:611): the LFP of the 3999 transient rows,
     # whose last W are the observation the reset returned
     tr = env.theta_record_transient
     assert tr.shape == (3999,)
     np.testing.assert_array_equal(tr[-env._v.W:].astype(np.float32), env.theta_state.ravel())
+    # ... and it is calc_lfp(sol_state[:-1]) (env.py:611), sampled rows
+    for s in (0, 1, 1000, len(ts) - 2):
+        _n, r = o.lfp(sol[s], env._v._g_rec[0])
+        assert r == env._v.get_attr("theta_record_transient")[0][s], s
+    # off: the reference attribute raises with the reason until the first step
+    env._v.sim.capture_transient_rows(False)
+    env.reset()
+    with pytest.raises(AttributeError, match="transient"):
+        env.sol_state
     env.close()

@@ -31,7 +31,7 @@ for round in $(seq 1 ${ROUNDS:-2}); do
     for set in "${SETV[@]}"; do
       f=$O/bench_${tn}_${si}_${round}.json
       (cd $t && KURA_LIB=${lib:+$R/$lib} timeout -k 10 300 python3 bench.py $set --cpu-seconds 0 > $f 2> ${f%.json}.err) || { echo "bench $tn [$set] failed"; exit 1; }
-      python3 -c "import json,sys;d=json.loads([l for l in open('$f') if l.startswith('{')][-1]);print('$tn','[$set]','r$round',round(d['value']),round(d['ms_per_step'],4),round(d['roofline']['frac'],4),round(d['roofline']['avg_kernel_ms'],4),round(d['extra'].get('reset_ms',0),1))" | tee -a $O/summary.txt
+      python3 -c "import json,sys;d=json.loads([l for l in open('$f') if l.startswith('{')][-1]);print('$tn','[$set]','r$round',round(d['value']),round(d['ms_per_step'],4),round(d['roofline']['frac'],4),round(d['roofline']['avg_kernel_ms'],4),round(d['extra'].get('reset_ms_warm') or d['extra'].get('reset_ms',0),1))" | tee -a $O/summary.txt
       si=$((si+1))
     done
   done

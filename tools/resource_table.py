@@ -3,7 +3,8 @@
 kura_kernels.hip with -Rpass-analysis=kernel-resource-usage (same flags as the
 production build) and prints one row per step/reset instantiation:
 VGPR / AGPR / SGPR / scratch bytes per lane / VGPR spills / LDS / occupancy.
-    python tools/resource_table.py > profiles/r03_resource_usage.txt"""
+    python tools/resource_table.py > profiles/r03_resource_usage.txt
+(KURA_RES_FLAGS="-DKURA_SAVE_SCALAR ..." adds defines: the table of an A/B variant)"""
 import os
 import re
 import subprocess
@@ -16,7 +17,7 @@ import __graft_entry__ as ge  # noqa: E402
 
 def main():
     src = os.path.join(ge.CSRC, "kura_kernels.hip")
-    flags = [f for f in ge.HIP_FLAGS if f not in ("-shared",)]
+    flags = [f for f in ge.HIP_FLAGS if f not in ("-shared",)] + os.environ.get("KURA_RES_FLAGS", "").split()
     cmd = [ge.HIPCC, *flags, "-Rpass-analysis=kernel-resource-usage", "-c", "-o", "/tmp/_kura_res.o", src]
     out = subprocess.run(cmd, capture_output=True, text=True, cwd=ge.CSRC).stderr
     rows, cur = [], None

@@ -9,7 +9,7 @@ checks the census of both builds lists the same functions and store counts
 in the same order).  For every site it prints the guarded
 stores and the source line each one comes from.
 
-    python tools/store_mask_sites.py [--out FILE]
+    python tools/store_mask_sites.py [--debug] [--out FILE]
 """
 from __future__ import annotations
 
@@ -27,11 +27,11 @@ import check_store_hazards as csh  # noqa: E402
 _LINE = re.compile(r"^; (/\S+?):(\d+)")
 
 
-def build_with_lines(out: str) -> None:
+def build_with_lines(out: str, extra=()) -> None:
     sys.path.insert(0, ROOT)
     import __graft_entry__ as g
     src = os.path.join(g.CSRC, "kura_kernels.hip")
-    subprocess.run([g.HIPCC, *g.HIP_FLAGS, "-gline-tables-only", "-o", out, src], check=True)
+    subprocess.run([g.HIPCC, *g.HIP_FLAGS, *extra, "-gline-tables-only", "-o", out, src], check=True)
 
 
 def parse_with_lines(text: str):
@@ -77,19 +77,21 @@ def census(lib: str, lines: bool):
 
 def main(argv):
     out = None
+    debug = "--debug" in argv   # libkura_debug.so (-DKURA_DEBUG) instead of libkura.so
+    argv = [a for a in argv if a != "--debug"]
     if argv[:1] == ["--out"]:
         out = argv[1]
-    shipped = os.path.join(ROOT, "dbs-gym_amd", "csrc", "libkura.so")
+    shipped = os.path.join(ROOT, "dbs-gym_amd", "csrc", "libkura_debug.so" if debug else "libkura.so")
     _, _, sites = census(shipped, False)
     with tempfile.TemporaryDirectory() as d:
         glib = os.path.join(d, "libkura_lines.so")
-        build_with_lines(glib)
+        build_with_lines(glib, ["-DKURA_DEBUG"] if debug else [])
         gfuncs, glocs, gsites = census(glib, True)
     # the same sites (function, guarded stores) in the same order; instruction
     # indices may shift by a few where the line tables move a scheduling boundary
     same = [(n, k) for n, _i, _v, k in sites] == [(n, k) for n, _i, _v, k in gsites]
     shift = max((abs(a[1] - b[1]) for a, b in zip(sites, gsites)), default=0)
-    lines = [f"shipped libkura.so: {len(sites)} sites, {sum(k for *_r, k in sites)} stores under a spilled exec mask",
+    lines = [f"shipped {os.path.basename(shipped)}: {len(sites)} sites, {sum(k for *_r, k in sites)} stores under a spilled exec mask",
              f"line-table build: {len(gsites)} sites -- same functions and store counts as the shipped build: {same} "
              f"(largest instruction-index shift {shift})", ""]
     fidx = {name: j for j, (name, _ins) in enumerate(gfuncs)}
