@@ -448,7 +448,7 @@ __device__ __forceinline__ void coupling_gemm_f32(const float* __restrict__ Xs, 
 // resident).  Same fragments, same MFMAs in the same order as
 // coupling_gemm_bf16x3, so the sums are identical; the fragment offsets are
 // scalar loads one k-block ahead of the refill they serve.  Used by the
-// reset (-DKURA_RESET_DEDUP): over its ~457 sweeps the workgroups of an XCD
+// reset (KURA_RESET_DEDUP): over its ~457 sweeps the workgroups of an XCD
 // drift apart and the 6 MiB streamed image misses L2.
 template <int TPW>
 __device__ __forceinline__ void coupling_gemm_bf16x3_dd(const float* __restrict__ Xs, const float* __restrict__ alpha_dd,
@@ -525,8 +525,11 @@ __device__ __forceinline__ void coupling_gemm(const float* __restrict__ Xs, cons
         coupling_gemm_f32<TPW>(Xs, alpha_sw, acc, dbg);
 }
 
+// the reset's GEMM reads the deduplicated alpha image (coupling_gemm_bf16x3_dd):
+// same box, warm B=4096 env0 reset 56.3 -> 53.3 ms, step unchanged
+// (profiles/r06_reset_dedup_ab.txt); -DKURA_RESET_DEDUP=0 streams the plain image
 #ifndef KURA_RESET_DEDUP
-#define KURA_RESET_DEDUP 0
+#define KURA_RESET_DEDUP 1
 #endif
 
 // Workgroup barrier that orders LDS only.  Inside a solve every workspace
