@@ -1488,6 +1488,19 @@ __device__ __forceinline__ void group_sum(DevParamsK& p, Part& pt, float (&vf)[N
     // wave 0 (a scalar branch): lanes >= E_WG get an offset past the
     // descriptor's range, which the hardware drops -- no exec-masked store
     // (hazards)
+#ifdef KURA_GROUPSUM_ATOMIC
+    // A/B form (round 5): relaxed agent-scope atomic stores by threads 0..15
+    if (tid < E_WG)
+        for (int k = 0; k < nk; ++k) {
+            __hip_atomic_store((gu32*)(xr + (part * RC + k) * E_WG + tid), __float_as_uint(vf[k]),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (with_d)
+                __hip_atomic_store((__attribute__((address_space(1))) unsigned long long*)(xd + (part * RC + k) *
+                                                                                              E_WG + tid),
+                                   (unsigned long long)__double_as_longlong(vd[k]), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+        }
+#else
     if (__builtin_amdgcn_readfirstlane(tid >> 6) == 0) {
         constexpr int kSc1 = 16;          // cache policy: sc1 (write-through to memory)
         constexpr int kDrop = 0x7ffffff0;
@@ -1507,6 +1520,7 @@ __device__ __forceinline__ void group_sum(DevParamsK& p, Part& pt, float (&vf)[N
             }
         }
     }
+#endif
     group_barrier(p, pt);
     if (tid < E_WG)
         for (int k = 0; k < nk; ++k) {
