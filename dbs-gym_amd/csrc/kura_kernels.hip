@@ -309,6 +309,12 @@ __device__ __forceinline__ void split_bf16x3(floatx4 lo, floatx4 hi, bf16x8& h1,
 }
 #endif
 
+// KURA_EXP_ALPHA (measurement builds only, wrong sums): 1 = every k-block
+// reads block 0's fragments (alpha L1-resident, same instructions), 2 = no
+// refill loads at all -- upper bounds of what alpha locality could gain
+#ifndef KURA_EXP_ALPHA
+#define KURA_EXP_ALPHA 0
+#endif
 template <int TPW>
 __device__ __forceinline__ void coupling_gemm_bf16x3(const float* __restrict__ Xs, const float* __restrict__ alpha_sw,
                                                      floatx16 (&acc)[TPW], unsigned long long* dbg = nullptr) {
@@ -329,6 +335,9 @@ __device__ __forceinline__ void coupling_gemm_bf16x3(const float* __restrict__ X
         (void*)((const char*)au + (size_t)wave * TPW * TSTRIDE), 0, TPW * TSTRIDE, 0x00020000);
     auto ld = [&](int t, int b, int p) -> bf16x8 {
         KDBG_CHECK(dbg, b >= 0 && b < NB && ((b * 3 + p) * 64 + lane) * 16 + t * TSTRIDE + 16 <= TPW * TSTRIDE);
+#if KURA_EXP_ALPHA == 1   // measurement only (wrong sums): every k-block reads block 0 -- alpha L1-resident
+        b = 0;
+#endif
         return __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rs, ((b * 3 + p) * 64 + lane) * 16,
                                                                                  t * TSTRIDE, 0));
     };
@@ -357,9 +366,13 @@ __device__ __forceinline__ void coupling_gemm_bf16x3(const float* __restrict__ X
             acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x1, a3[d][t], acc[t], 0, 0, 0);
             acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x2, a2[d][t], acc[t], 0, 0, 0);
             acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x3, a1[d][t], acc[t], 0, 0, 0);
+#if KURA_EXP_ALPHA != 2   // (measurement only, wrong sums: =2 keeps the first two blocks' fragments, no alpha traffic)
             a1[d][t] = ld(t, bn, 0);
             a2[d][t] = ld(t, bn, 1);
             a3[d][t] = ld(t, bn, 2);
+#else
+            (void)bn;
+#endif
         }
         __builtin_amdgcn_sched_barrier(0);
     };
@@ -531,6 +544,7 @@ __device__ __forceinline__ void coupling_gemm(const float* __restrict__ Xs, cons
 #ifndef KURA_RESET_DEDUP
 #define KURA_RESET_DEDUP 1
 #endif
+
 
 // Workgroup barrier that orders LDS only.  Inside a solve every workspace
 // record (R) is written and read back by the same lane (MFMA-layout
