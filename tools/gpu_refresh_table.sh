@@ -18,6 +18,6 @@ timeout -k 10 300 python bench.py --steps 5 --warmup 1 --cpu-seconds 0 --osc 819
 timeout -k 10 300 python bench.py --steps 5 --warmup 1 --cpu-seconds 0 --osc 8192 --envs 128 > $O/stress_strong.json 2> $O/stress_strong.err
 timeout -k 10 400 python bench.py --steps 10 --warmup 2 --cpu-seconds 0 --episode > $O/episode.json 2> $O/episode.err
 for f in env0_r1 env0_r1_f32 env1_r1 env1_r2 env0_r3 env2_rk stress_weak stress_strong episode; do
-  python -c "import json;d=json.loads(open('$O/$f.json').readline());print('$f', round(d['value']), round(d['ms_per_step'],3), round(d['roofline']['frac'],4), d['dtype'], d.get('extra',{}).get('episode',{}).get('rate_vs_steady'))"
+  python -c "import json;d=json.loads(open('$O/$f.json').readline());print('$f', round(d['value']), round(d['ms_per_step'],3), round(d['roofline']['frac'],4), d['dtype'], d.get('extra',{}).get('episode',{}).get('episode_vs_steady'))"
 done
 echo ALLDONE
