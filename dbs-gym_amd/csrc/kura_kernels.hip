@@ -311,7 +311,10 @@ __device__ __forceinline__ void split_bf16x3(floatx4 lo, floatx4 hi, bf16x8& h1,
 
 // KURA_EXP_ALPHA (measurement builds only, wrong sums): 1 = every k-block
 // reads block 0's fragments (alpha L1-resident, same instructions), 2 = no
-// refill loads at all -- upper bounds of what alpha locality could gain
+// refill loads at all -- upper bounds of what alpha locality could gain;
+// 3 = the fragments gathered from a grid-displacement table in LDS (8 KB
+// after the operand, filled with bf16(0.5) parts: the access pattern and
+// instruction mix of an exact table gather with 64 of its 128 classes)
 #ifndef KURA_EXP_ALPHA
 #define KURA_EXP_ALPHA 0
 #endif
@@ -341,6 +344,37 @@ __device__ __forceinline__ void coupling_gemm_bf16x3(const float* __restrict__ X
         return __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rs, ((b * 3 + p) * 64 + lane) * 16,
                                                                                  t * TSTRIDE, 0));
     };
+#if KURA_EXP_ALPHA == 3
+    typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
+    u32x2_t* tab = reinterpret_cast<u32x2_t*>(const_cast<float*>(Xs) + xs_floats(N));
+    for (int i = lane; i < 1024; i += 64) tab[i] = u32x2_t{0x3F00u, 0u};   // each wave writes the whole table
+    const int j0 = 7 - (lane & 7) + (lane >> 5);
+    int xc[TPW], zc[TPW];
+#pragma unroll
+    for (int t = 0; t < TPW; ++t) {
+        const int line = 4 * (wave * TPW + t) + ((lane & 31) >> 3);
+        xc[t] = line & 15;
+        zc[t] = line >> 4;
+    }
+    auto gth = [&](int t, int b, bf16x8& q1, bf16x8& q2, bf16x8& q3) __attribute__((always_inline)) {
+        const int xk = (2 * b) & 15, zk = (2 * b) >> 4;
+        const int dz = __builtin_abs(zc[t] - zk) * 16;
+        const int c0 = (dz + __builtin_abs(xc[t] - xk)) & 63, c1 = (dz + __builtin_abs(xc[t] - xk - 1)) & 63;
+        const u32x2_t* r0 = tab + c0 * 16 + j0;
+        const u32x2_t* r1 = tab + c1 * 16 + j0;
+        const u32x2_t e[8] = {r0[0], r0[2], r0[4], r0[6], r1[0], r1[2], r1[4], r1[6]};
+        u32x4 w1, w2, w3;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            w1[q] = __builtin_amdgcn_perm(e[2 * q + 1].x, e[2 * q].x, 0x05040100u);
+            w2[q] = __builtin_amdgcn_perm(e[2 * q + 1].x, e[2 * q].x, 0x07060302u);
+            w3[q] = __builtin_amdgcn_perm(e[2 * q + 1].y, e[2 * q].y, 0x05040100u);
+        }
+        q1 = __builtin_bit_cast(bf16x8, w1);
+        q2 = __builtin_bit_cast(bf16x8, w2);
+        q3 = __builtin_bit_cast(bf16x8, w3);
+    };
+#endif
     // two register sets per tile: block b+2's parts load right after block
     // b's MFMAs, a whole block of cover (one set: the loads issue after the
     // block's last x3*a1 and the next block's first MFMA waits on them;
@@ -350,9 +384,13 @@ __device__ __forceinline__ void coupling_gemm_bf16x3(const float* __restrict__ X
     for (int d = 0; d < 2; ++d)
 #pragma unroll
         for (int t = 0; t < TPW; ++t) {
+#if KURA_EXP_ALPHA == 3
+            gth(t, d, a1[d][t], a2[d][t], a3[d][t]);
+#else
             a1[d][t] = ld(t, d < NB ? d : NB - 1, 0);
             a2[d][t] = ld(t, d < NB ? d : NB - 1, 1);
             a3[d][t] = ld(t, d < NB ? d : NB - 1, 2);
+#endif
         }
     auto blk = [&](int b, int d) __attribute__((always_inline)) {
         bf16x8 x1, x2, x3;
@@ -366,7 +404,9 @@ __device__ __forceinline__ void coupling_gemm_bf16x3(const float* __restrict__ X
             acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x1, a3[d][t], acc[t], 0, 0, 0);
             acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x2, a2[d][t], acc[t], 0, 0, 0);
             acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x3, a1[d][t], acc[t], 0, 0, 0);
-#if KURA_EXP_ALPHA != 2   // (measurement only, wrong sums: =2 keeps the first two blocks' fragments, no alpha traffic)
+#if KURA_EXP_ALPHA == 3
+            gth(t, bn, a1[d][t], a2[d][t], a3[d][t]);
+#elif KURA_EXP_ALPHA != 2   // (measurement only, wrong sums: =2 keeps the first two blocks' fragments, no alpha traffic)
             a1[d][t] = ld(t, bn, 0);
             a2[d][t] = ld(t, bn, 1);
             a3[d][t] = ld(t, bn, 2);
