@@ -313,8 +313,9 @@ __device__ __forceinline__ void split_bf16x3(floatx4 lo, floatx4 hi, bf16x8& h1,
 // reads block 0's fragments (alpha L1-resident, same instructions), 2 = no
 // refill loads at all -- upper bounds of what alpha locality could gain;
 // 3 = the fragments gathered from a grid-displacement table in LDS (8 KB
-// after the operand, filled with bf16(0.5) parts: the access pattern and
-// instruction mix of an exact table gather with 64 of its 128 classes)
+// after the operand, filled with split hashed values: the access pattern,
+// instruction mix and operand bit density of an exact table gather with 64
+// of its 128 classes)
 #ifndef KURA_EXP_ALPHA
 #define KURA_EXP_ALPHA 0
 #endif
@@ -347,7 +348,22 @@ __device__ __forceinline__ void coupling_gemm_bf16x3(const float* __restrict__ X
 #if KURA_EXP_ALPHA == 3
     typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
     u32x2_t* tab = reinterpret_cast<u32x2_t*>(const_cast<float*>(Xs) + xs_floats(N));
-    for (int i = lane; i < 1024; i += 64) tab[i] = u32x2_t{0x3F00u, 0u};   // each wave writes the whole table
+    // each wave writes the whole table: three-way bf16 splits of hashed values
+    // in (-0.9, 0.9), so the MFMA operands carry as many set bits as real alpha
+    for (int i = lane; i < 1024; i += 64) {
+        unsigned hs = (unsigned)(i + 1) * 2654435761u;
+        hs ^= hs >> 15;
+        hs *= 2246822519u;
+        hs ^= hs >> 13;
+        const float v = ((float)(hs & 0xffffffu) / 8388608.0f - 1.0f) * 0.9f;
+        const __bf16 a = (__bf16)v;
+        const float r1 = v - (float)a;
+        const __bf16 b = (__bf16)r1;
+        const __bf16 c = (__bf16)(r1 - (float)b);
+        tab[i] = u32x2_t{(unsigned)__builtin_bit_cast(unsigned short, a) |
+                             ((unsigned)__builtin_bit_cast(unsigned short, b) << 16),
+                         (unsigned)__builtin_bit_cast(unsigned short, c)};
+    }
     const int j0 = 7 - (lane & 7) + (lane >> 5);
     int xc[TPW], zc[TPW];
 #pragma unroll
