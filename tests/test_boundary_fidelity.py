@@ -81,3 +81,26 @@ def test_single_env_sol_state_rows():
     with pytest.raises(AttributeError, match="transient"):
         env.sol_state
     env.close()
+
+
+@pytest.mark.gpu
+def test_transient_rows_beyond_32bit_offsets_are_rejected():
+    """kura_set_transient_rows refuses a transient whose rows for one 16-env
+    group exceed the save passes' 32-bit byte offsets (N=8192, 6000 rows:
+    3.1 GB per group) instead of wrapping them."""
+    import ctypes
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from helpers import make_case
+    sim_mod = importlib.import_module("dbs-gym_amd.sim")
+    cfg = make_case("env0", 8192, 16)[0]
+    cfg.transient_len = 300.0
+    sim = sim_mod.KuraSim(cfg, 0)
+    try:
+        assert sim.lib.kura_transient_len(sim._h) == len(np.arange(0.0, 300.0, cfg.dt))
+        rc = sim.lib.kura_set_transient_rows(sim._h, ctypes.c_void_p(256))   # rejected before any use
+        assert rc != 0 and b"2 GiB" in sim.lib.kura_last_error()
+        assert sim.lib.kura_set_transient_rows(sim._h, None) == 0
+    finally:
+        sim.close()
