@@ -315,7 +315,9 @@ __device__ __forceinline__ void split_bf16x3(floatx4 lo, floatx4 hi, bf16x8& h1,
 // 3 = the fragments gathered from a grid-displacement table in LDS (8 KB
 // after the operand, filled with split hashed values: the access pattern,
 // instruction mix and operand bit density of an exact table gather with 64
-// of its 128 classes)
+// of its 128 classes).  KURA_EXP_ORDER (measurement builds only, a different
+// accumulation order than the oracle's): 1 / 2 group the six products by
+// their A / B operand -- does MFMA operand switching cost power here?
 #ifndef KURA_EXP_ALPHA
 #define KURA_EXP_ALPHA 0
 #endif
@@ -414,12 +416,28 @@ __device__ __forceinline__ void coupling_gemm_bf16x3(const float* __restrict__ X
         const int bn = b + 2 < NB ? b + 2 : NB - 1;
 #pragma unroll
         for (int t = 0; t < TPW; ++t) {
+#if KURA_EXP_ORDER == 1   // measurement only (a different accumulation order): A operand held for 3, 2, 1 MFMAs
+            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x1, a1[d][t], acc[t], 0, 0, 0);
+            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x1, a2[d][t], acc[t], 0, 0, 0);
+            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x1, a3[d][t], acc[t], 0, 0, 0);
+            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x2, a1[d][t], acc[t], 0, 0, 0);
+            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x2, a2[d][t], acc[t], 0, 0, 0);
+            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x3, a1[d][t], acc[t], 0, 0, 0);
+#elif KURA_EXP_ORDER == 2   // measurement only: B operand held for 3, 2, 1 MFMAs
+            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x1, a1[d][t], acc[t], 0, 0, 0);
+            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x2, a1[d][t], acc[t], 0, 0, 0);
+            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x3, a1[d][t], acc[t], 0, 0, 0);
+            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x1, a2[d][t], acc[t], 0, 0, 0);
+            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x2, a2[d][t], acc[t], 0, 0, 0);
+            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x1, a3[d][t], acc[t], 0, 0, 0);
+#else
             acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x1, a1[d][t], acc[t], 0, 0, 0);
             acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x1, a2[d][t], acc[t], 0, 0, 0);
             acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x2, a1[d][t], acc[t], 0, 0, 0);
             acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x1, a3[d][t], acc[t], 0, 0, 0);
             acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x2, a2[d][t], acc[t], 0, 0, 0);
             acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x3, a1[d][t], acc[t], 0, 0, 0);
+#endif
 #if KURA_EXP_ALPHA == 3
             gth(t, bn, a1[d][t], a2[d][t], a3[d][t]);
 #elif KURA_EXP_ALPHA != 2   // (measurement only, wrong sums: =2 keeps the first two blocks' fragments, no alpha traffic)
