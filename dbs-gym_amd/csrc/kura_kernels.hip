@@ -67,6 +67,7 @@ struct DevParams {
     float rtol, atol, kn, dt0;
     const float* alpha_sw;  // B-fragment swizzled coupling
     const float* alpha_dd;  // BF16X3, N <= 1024: the deduplicated image too (the reset's GEMM, -DKURA_RESET_DEDUP)
+    unsigned alpha_dd_bytes;  // its size (the GEMM's descriptor range)
     const float* omega;     // [B][N]
     const float* kn_env;    // [B] float32(K_b / N), per-env coupling gain
     const double* g_stim;   // [B][n_elec][N]
@@ -539,7 +540,7 @@ __device__ __forceinline__ void coupling_gemm_f32(const float* __restrict__ Xs, 
 // drift apart and the 6 MiB streamed image misses L2.
 template <int TPW>
 __device__ __forceinline__ void coupling_gemm_bf16x3_dd(const float* __restrict__ Xs, const float* __restrict__ alpha_dd,
-                                                        floatx16 (&acc)[TPW]) {
+                                                        unsigned img_bytes, floatx16 (&acc)[TPW]) {
     constexpr int N = TPW * 32 * NWAVES;
     constexpr int NB = N / 16, NT = N / 32;
     constexpr unsigned FRAG = 3 * 64 * 16;
@@ -552,8 +553,9 @@ __device__ __forceinline__ void coupling_gemm_bf16x3_dd(const float* __restrict_
         for (int r = 0; r < 16; ++r) acc[t][r] = 0.0f;
     const floatx4* xs4 = reinterpret_cast<const floatx4*>(Xs + (lane >> 5) * XS_HALF + (lane & 31) * 4);
     const float* au = uniform_ptr(alpha_dd);
-    const unsigned IMG = (unsigned)NT * NB * 4u + (unsigned)NT * NB * FRAG;   // bound: every fragment distinct
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)au, 0, IMG, 0x00020000);
+    (void)FRAG;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)au, 0, __builtin_amdgcn_readfirstlane(img_bytes), 0x00020000);   // map + distinct fragments
     // the map through the constant address space: scalar loads (s_load_dword)
     typedef const __attribute__((address_space(4))) int cint;
     cint* mp = reinterpret_cast<cint*>(reinterpret_cast<uintptr_t>(au)) + wave * TPW;   // map row b: mp[b * NT + t]
@@ -2459,7 +2461,7 @@ __device__ KURA_SOLVE_ATTR void solve_wg(DevParamsK& __restrict__ pin, float* Xs
 #else
 #if KURA_RESET_DEDUP
             if constexpr (SP && RS)
-                coupling_gemm_bf16x3_dd<TPW>(Xs, p.alpha_dd, acc);
+                coupling_gemm_bf16x3_dd<TPW>(Xs, p.alpha_dd, p.alpha_dd_bytes, acc);
             else
 #endif
                 coupling_gemm<TPW, SP>(Xs, p.alpha_sw, acc);
